@@ -1,0 +1,299 @@
+#!/usr/bin/env python3
+"""LLaMA-7B SpecInfer (LLaMA-68M SSM) decoded tokens/s on MI355X.
+
+Workload (BASELINE.json metric / SURVEY.md §8d): 8 requests, prompt = BOS +
+127 ids (splitmix64, seed 20250117), 128 decoded tokens each (max_length
+256), max_tokens_per_batch 1024, max_spec_tree_token_num 23, tree widths
+(1,1,3), 8 SSM steps per verify; synthetic seeded weights (no checkpoints
+offline).  One "step" = one generate() of the whole 8-request batch.
+N GPUs = tensor parallelism over N ranks (one process per GPU, RCCL), the SSM
+replicated per rank.  value = decoded tokens of all requests / wall time
+(max over ranks).
+
+The process never imports torch (torch bundles a second copy of the HIP
+runtime); the multi-rank control plane (unique-id broadcast, barrier,
+max-reduce of times) is a small TCP exchange on 127.0.0.1.
+"""
+import argparse
+import json
+import os
+import socket
+import statistics
+import struct
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import flexflow_amd as fa  # noqa: E402  (load libffmi before anything else)
+
+LLAMA_7B = dict(num_layers=32, vocab_size=32000, num_heads=32, num_kv_heads=32, hidden=4096,
+                intermediate=11008, rms_eps=1e-6, rope_theta=10000.0)
+LLAMA_68M = dict(num_layers=2, vocab_size=32000, num_heads=12, num_kv_heads=12, hidden=768,
+                 intermediate=3072, rms_eps=1e-6, rope_theta=10000.0)
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+M64 = (1 << 64) - 1
+
+
+def splitmix64_stream(seed):
+    x = seed & M64
+    while True:
+        x = (x + 0x9E3779B97F4A7C15) & M64
+        z = x
+        z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+        z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+        yield z ^ (z >> 31)
+
+
+def make_prompts(n, length, vocab, seed=20250117):
+    g = splitmix64_stream(seed)
+    return [[3 + next(g) % (vocab - 3) for _ in range(length)] for _ in range(n)]
+
+
+class Ctrl:
+    """Rank-0-hub TCP control plane (bytes broadcast, barrier, max)."""
+
+    def __init__(self, rank, world, port):
+        self.rank, self.world = rank, world
+        self.peers = []
+        if world == 1:
+            return
+        if rank == 0:
+            srv = socket.socket(socket.AF_INET, socket.SOCK_STREAM)
+            srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
+            srv.bind(("127.0.0.1", port))
+            srv.listen(world)
+            for _ in range(world - 1):
+                c, _ = srv.accept()
+                self.peers.append(c)
+            srv.close()
+        else:
+            deadline = time.time() + 300
+            while True:
+                try:
+                    self.sock = socket.create_connection(("127.0.0.1", port), timeout=300)
+                    break
+                except OSError:
+                    if time.time() > deadline:
+                        raise
+                    time.sleep(0.2)
+
+    @staticmethod
+    def _recv(s, n):
+        b = b""
+        while len(b) < n:
+            chunk = s.recv(n - len(b))
+            if not chunk:
+                raise ConnectionError("control plane closed")
+            b += chunk
+        return b
+
+    def bcast(self, data: bytes) -> bytes:
+        if self.world == 1:
+            return data
+        if self.rank == 0:
+            for p in self.peers:
+                p.sendall(struct.pack("<I", len(data)) + data)
+            return data
+        n = struct.unpack("<I", self._recv(self.sock, 4))[0]
+        return self._recv(self.sock, n)
+
+    def max(self, v: float) -> float:
+        if self.world == 1:
+            return v
+        if self.rank == 0:
+            vals = [v] + [struct.unpack("<d", self._recv(p, 8))[0] for p in self.peers]
+            m = max(vals)
+            for p in self.peers:
+                p.sendall(struct.pack("<d", m))
+            return m
+        self.sock.sendall(struct.pack("<d", v))
+        return struct.unpack("<d", self._recv(self.sock, 8))[0]
+
+    def barrier(self):
+        self.max(0.0)
+
+
+def device_sync():
+    import ctypes
+    h = ctypes.CDLL("libamdhip64.so.7")
+    assert h.hipDeviceSynchronize() == 0
+
+
+def run_generate(rm, llm, prompts, max_length, spec):
+    res = fa.generate(rm, llm, prompts, max_length=max_length, spec=spec)
+    new = sum(len(r.output_tokens) - len(r.input_tokens) for r in res)
+    lat = [(r.latency_us / max(1, len(r.output_tokens) - len(r.input_tokens))) for r in res]
+    return new, lat, res
+
+
+def cpu_baseline(prompt_len=4, steps=4, batch=8):
+    """The CPU restatement (oracle/, test infrastructure) timed on the host:
+    LLaMA-7B fp16-semantics incremental decoding, batch 8, `steps` batched
+    decode steps after a short prompt (a bounded sample of the workload)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+
+    import oracle_lib as O
+    m = O.Model(LLAMA_7B, 20250117, fp16=1, max_requests=batch, max_seq=prompt_len + steps + 2)
+    prompts = make_prompts(batch, prompt_len, LLAMA_7B["vocab_size"], seed=7)
+    reqs = np.arange(batch, dtype=np.int32)
+    for p in range(prompt_len):  # untimed prefill, one batched step per position
+        m.decode_batch(reqs, [pr[p] for pr in prompts], [p] * batch)
+    toks = [pr[-1] for pr in prompts]
+    t0 = time.time()
+    for s in range(steps):
+        logits = m.decode_batch(reqs, toks, [prompt_len + s] * batch)
+        toks = O.softmax_argmax(logits, fp16=1)[0].tolist()
+    dt = time.time() - t0
+    return dict(value=round(batch * steps / dt, 3), unit="decoded tokens/s",
+                cores=int(O.lib().orc_num_threads()), kind="port",
+                sample=f"oracle LLaMA-7B incr decoding, batch {batch}, {steps} decode steps "
+                       f"after a {prompt_len}-token prompt, {dt:.1f}s")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--mode", choices=["spec", "incr"], default="spec")
+    ap.add_argument("--batch", type=int, default=8)
+    ap.add_argument("--prefill", type=int, default=128)
+    ap.add_argument("--decode", type=int, default=128)
+    ap.add_argument("--max-tokens-per-batch", type=int, default=1024)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-incr", action="store_true", help="skip the incr-decoding side run")
+    ap.add_argument("--profile", type=int, default=1, help="op profiling level in timed steps")
+    ap.add_argument("--layers", type=int, default=0, help="override LLM layer count (debug)")
+    args = ap.parse_args()
+
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", args.gpus))
+    local = int(os.environ.get("LOCAL_RANK", rank))
+    if world != args.gpus:
+        raise SystemExit(f"WORLD_SIZE {world} != --gpus {args.gpus}")
+    port = int(os.environ.get("MASTER_PORT", 29500)) + 31
+    ctrl = Ctrl(rank, world, port)
+    fa.set_device(local)
+    comm = None
+    if world > 1:
+        uid = ctrl.bcast(fa.Comm.unique_id() if rank == 0 else b"")
+        comm = fa.Comm(uid, world, rank)
+
+    llm_cfg = dict(LLAMA_7B)
+    if args.layers:
+        llm_cfg["num_layers"] = args.layers
+    B, P, D = args.batch, args.prefill, args.decode
+    max_len = P + D
+    mtb = args.max_tokens_per_batch
+    tree = 23
+    widths = (1, 1, 3)
+    prompts = make_prompts(B, P - 1, llm_cfg["vocab_size"])  # + BOS = P tokens
+    verify_cap = mtb + tree * B
+
+    spec = args.mode == "spec"
+    rm_kw = dict(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                 max_spec_tree_token_num=tree, max_sequence_length=max(512, max_len + 1))
+    t_init = time.time()
+    if spec:
+        llm = fa.Model(llm_cfg, "tree", max_requests=B, max_tokens=verify_cap,
+                       max_seq_len=rm_kw["max_sequence_length"], max_tree_tokens=tree,
+                       weight_seed=20250117, tp_rank=rank, tp_size=world, comm=comm)
+        ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=verify_cap,
+                       max_seq_len=rm_kw["max_sequence_length"], max_tree_tokens=tree,
+                       weight_seed=68)
+        rm = fa.RequestManager(spec_tree_width=widths, **rm_kw)
+        rm.register_ssm_model(ssm)
+    else:
+        llm = fa.Model(llm_cfg, "inc", max_requests=B, max_tokens=mtb,
+                       max_seq_len=rm_kw["max_sequence_length"], weight_seed=20250117,
+                       tp_rank=rank, tp_size=world, comm=comm)
+        rm = fa.RequestManager(**rm_kw)
+    init_s = time.time() - t_init
+
+    for _ in range(args.warmup):
+        run_generate(rm, llm, prompts, max_len, spec)
+    if args.profile:
+        llm.set_profiling(args.profile)
+    ctrl.barrier()
+    device_sync()
+    t0 = time.time()
+    new_tokens, lats, llm_steps, ssm_steps = 0, [], 0, 0
+    committed = 0
+    for _ in range(args.steps):
+        n, lat, res = run_generate(rm, llm, prompts, max_len, spec)
+        st = rm.stats()
+        new_tokens += n
+        lats += lat
+        llm_steps += st.llm_steps
+        ssm_steps += st.ssm_steps
+        committed += st.tokens_committed
+    device_sync()
+    ctrl.barrier()
+    elapsed = ctrl.max(time.time() - t0)
+    ops = llm.op_stats() if args.profile else {}
+    if args.profile:
+        llm.set_profiling(0)
+
+    value = new_tokens / elapsed  # every rank decodes the same requests (TP)
+    out = {
+        "metric": "decoded tokens/s (LLaMA-7B SpecInfer, LLaMA-68M SSM)" if spec else
+                  "decoded tokens/s (LLaMA-7B incremental decoding)",
+        "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
+        "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f16",
+        "data": "synthetic (seeded random weights and prompts)",
+        "config": {"workload": ("llama7b_specinfer_llama68m" if spec else "llama7b_incr") +
+                   f"_b{B}_p{P}_d{D}", "model": "LLaMA-7B (random init)",
+                   "ssm": "LLaMA-68M (random init)" if spec else None,
+                   "global_batch": B, "prefill": P, "decode": D, "seq_len": max_len,
+                   "parallelism": f"tp{world}", "tree_widths": list(widths) if spec else None,
+                   "max_tokens_per_batch": mtb, "layers": llm_cfg["num_layers"]},
+        "p50_token_latency_ms": round(statistics.median(lats) / 1000.0, 3),
+        "llm_steps_per_generate": llm_steps / args.steps,
+        "ssm_steps_per_generate": ssm_steps / args.steps,
+        "init_s": round(init_s, 1),
+    }
+    if spec:
+        out["accepted_tokens_per_verify"] = round(committed / max(1, llm_steps), 3)
+    # roofline of the dominant kernel: the weight-streaming GEMM with the
+    # largest sampled time (HIP events on the model stream, timed region)
+    gemms = {k: v for k, v in ops.items() if k.startswith("gemm") and v["ms"] > 0}
+    if gemms:
+        k = max(gemms, key=lambda x: gemms[x]["ms"])
+        g = gemms[k]
+        ach = g["bytes"] / (g["ms"] * 1e-3) / 1e9
+        out["roofline"] = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                           "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                           "kernel": k, "launches_sampled": g["launches"],
+                           "avg_launch_us": round(1000 * g["ms"] / g["launches"], 2),
+                           "bytes_per_launch": round(g["bytes"] / g["launches"])}
+        out["op_breakdown_sampled"] = {
+            kk: {"avg_us": round(1000 * v["ms"] / v["launches"], 2),
+                 "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
+                 "launches": v["launches"]} for kk, v in ops.items()}
+    if rank == 0 and world == 1 and spec and not args.no_incr:
+        inc = fa.Model(llm_cfg, "inc", max_requests=B, max_tokens=mtb,
+                       max_seq_len=rm_kw["max_sequence_length"], weight_seed=20250117)
+        rmi = fa.RequestManager(**rm_kw)
+        run_generate(rmi, inc, prompts, max_len, False)  # warm
+        t1 = time.time()
+        n, lat, _ = run_generate(rmi, inc, prompts, max_len, False)
+        dt = time.time() - t1
+        out["incr_decoding"] = {"value": round(n / dt, 2), "unit": "tokens/s",
+                                "p50_token_latency_ms": round(statistics.median(lat) / 1000, 3),
+                                "llm_steps": rmi.stats().llm_steps}
+        inc.close()
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline()
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    llm.close()
+    if comm:
+        comm.close()
+
+
+if __name__ == "__main__":
+    main()

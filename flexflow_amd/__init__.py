@@ -1,0 +1,11 @@
+"""flexflow_amd -- MI355X-native SpecInfer hot path (libffmi.so).
+
+Import order matters on ROCm: load libffmi.so before torch so both share one
+HIP runtime (same SONAME libamdhip64.so.7).
+"""
+from . import ffmi  # noqa: F401
+from .serve import (Comm, GenerationResult, HashModel, Model, RequestManager,  # noqa: F401
+                    generate, set_device)
+
+__all__ = ["ffmi", "Comm", "GenerationResult", "HashModel", "Model", "RequestManager",
+           "generate", "set_device"]

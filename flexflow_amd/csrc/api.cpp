@@ -1,0 +1,381 @@
+// api.cpp -- C ABI of the kernel-level boundary (include/ffmi.h).
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <cmath>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "ffmi_internal.h"
+
+static thread_local std::string g_last_error;
+
+void ffmi_set_last_error(const char *msg, const char *file, int line) {
+  char buf[512];
+  snprintf(buf, sizeof(buf), "%s (%s:%d)", msg, file, line);
+  g_last_error = buf;
+  if (getenv("FFMI_VERBOSE_ERRORS")) fprintf(stderr, "[ffmi] error: %s\n", buf);
+}
+
+extern "C" const char *ffmi_last_error(void) { return g_last_error.c_str(); }
+
+extern "C" const char *ffmi_status_str(ffmi_status s) {
+  switch (s) {
+    case FFMI_OK: return "ok";
+    case FFMI_ERR_INVALID: return "invalid argument";
+    case FFMI_ERR_HIP: return "hip error";
+    case FFMI_ERR_NCCL: return "rccl error";
+    case FFMI_ERR_OOM: return "out of device memory";
+    case FFMI_ERR_UNSUPPORTED: return "unsupported";
+    case FFMI_ERR_NO_DEVICE: return "no gfx950 device";
+  }
+  return "unknown";
+}
+
+extern "C" const char *ffmi_version(void) { return "ffmi 0.1 (gfx950)"; }
+
+// ---------------------------------------------------------------------------
+// batch metadata
+// ---------------------------------------------------------------------------
+static size_t align16(size_t x) { return (x + 15) & ~(size_t)15; }
+
+extern "C" ffmi_status ffmi_batch_create(int max_tokens, int max_requests, ffmi_batch_dev **out) {
+  FFMI_CHECK(max_tokens > 0 && max_requests > 0 && out, FFMI_ERR_INVALID);
+  ffmi_batch_dev *b = new ffmi_batch_dev();
+  b->max_tokens = max_tokens;
+  b->max_requests = max_requests;
+  // header + tokens + work (<= tokens) + commits (<= tokens) + masks
+  b->cap = align16(sizeof(ffmi::BatchHeader)) + align16((size_t)max_tokens * sizeof(ffmi_token_info)) +
+           align16((size_t)max_tokens * sizeof(ffmi_attn_work)) +
+           align16((size_t)max_tokens * sizeof(ffmi_commit_info)) +
+           align16((size_t)max_requests * FFMI_MAX_TREE * sizeof(uint64_t)) + 64;
+  if (hipHostMalloc((void **)&b->host, b->cap, hipHostMallocDefault) != hipSuccess ||
+      hipMalloc((void **)&b->dev, b->cap) != hipSuccess) {
+    delete b;
+    ffmi_set_last_error("batch alloc", __FILE__, __LINE__);
+    return FFMI_ERR_OOM;
+  }
+  memset(b->host, 0, b->cap);
+  FFMI_HIP(hipMemset(b->dev, 0, b->cap));
+  FFMI_HIP(hipEventCreateWithFlags(&b->uploaded, hipEventDisableTiming));
+  *out = b;
+  return FFMI_OK;
+}
+
+extern "C" void ffmi_batch_destroy(ffmi_batch_dev *b) {
+  if (!b) return;
+  if (b->uploaded) {
+    (void)hipEventSynchronize(b->uploaded);
+    (void)hipEventDestroy(b->uploaded);
+  }
+  if (b->host) (void)hipHostFree(b->host);
+  if (b->dev) (void)hipFree(b->dev);
+  delete b;
+}
+
+extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_desc *d,
+                                         ffmi_stream stream) {
+  FFMI_CHECK(b && d, FFMI_ERR_INVALID);
+  FFMI_CHECK(d->num_tokens >= 0 && d->num_tokens <= b->max_tokens, FFMI_ERR_INVALID);
+  FFMI_CHECK(d->num_work >= 0 && d->num_work <= b->max_tokens, FFMI_ERR_INVALID);
+  FFMI_CHECK(d->num_commits >= 0 && d->num_commits <= b->max_tokens, FFMI_ERR_INVALID);
+  FFMI_CHECK(d->num_mask_reqs >= 0 && d->num_mask_reqs <= b->max_requests, FFMI_ERR_INVALID);
+  // the pinned staging may still be read by the previous async copy
+  FFMI_HIP(hipEventSynchronize(b->uploaded));
+  ffmi::BatchHeader h;
+  size_t off = align16(sizeof(h));
+  h.num_tokens = d->num_tokens;
+  h.num_work = d->num_work;
+  h.num_commits = d->num_commits;
+  h.num_mask_reqs = d->num_mask_reqs;
+  h.off_tokens = (int)off;
+  memcpy(b->host + off, d->tokens, d->num_tokens * sizeof(ffmi_token_info));
+  off += align16(d->num_tokens * sizeof(ffmi_token_info));
+  h.off_work = (int)off;
+  memcpy(b->host + off, d->work, d->num_work * sizeof(ffmi_attn_work));
+  off += align16(d->num_work * sizeof(ffmi_attn_work));
+  h.off_commits = (int)off;
+  if (d->num_commits) memcpy(b->host + off, d->commits, d->num_commits * sizeof(ffmi_commit_info));
+  off += align16(d->num_commits * sizeof(ffmi_commit_info));
+  h.off_masks = (int)off;
+  if (d->num_mask_reqs)
+    memcpy(b->host + off, d->masks, (size_t)d->num_mask_reqs * FFMI_MAX_TREE * sizeof(uint64_t));
+  off += (size_t)d->num_mask_reqs * FFMI_MAX_TREE * sizeof(uint64_t);
+  memcpy(b->host, &h, sizeof(h));
+  FFMI_CHECK(off <= b->cap, FFMI_ERR_INVALID);
+  FFMI_HIP(hipMemcpyAsync(b->dev, b->host, off, hipMemcpyHostToDevice, (hipStream_t)stream));
+  FFMI_HIP(hipEventRecord(b->uploaded, (hipStream_t)stream));
+  b->num_tokens = d->num_tokens;
+  b->num_work = d->num_work;
+  b->num_commits = d->num_commits;
+  b->num_mask_reqs = d->num_mask_reqs;
+  return FFMI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// attention handles
+// ---------------------------------------------------------------------------
+struct ffmi_attn {
+  ffmi_attn_cfg cfg;
+  int slots = 0;
+  uint16_t *kc = nullptr, *vc = nullptr, *qbuf = nullptr, *stage = nullptr;
+  float *rope = nullptr;
+};
+
+// cos/sin table, same arithmetic as the reference's apply_rotary_embedding_hf
+// (inc_multihead_self_attention.cu:701-703): freq = pos * (1.0 /
+// pow(theta, 2i/d)) in the float/double mix used there, cos/sin in f32.
+static void rope_table(std::vector<float> &tab, int max_pos, int d, float theta) {
+  const int h = d / 2;
+  std::vector<double> inv(h);
+  for (int i = 0; i < h; ++i) {
+    volatile float ex = (float)2 * (float)i / (float)d;
+    inv[i] = 1.0 / (double)powf(theta, ex);
+  }
+  tab.resize((size_t)max_pos * d);
+  for (int p = 0; p < max_pos; ++p)
+    for (int i = 0; i < h; ++i) {
+      volatile float freq = (float)((double)p * inv[i]);
+      tab[((size_t)p * h + i) * 2 + 0] = cosf(freq);
+      tab[((size_t)p * h + i) * 2 + 1] = sinf(freq);
+    }
+}
+
+extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **out) {
+  FFMI_CHECK(cfg && out, FFMI_ERR_INVALID);
+  FFMI_CHECK(cfg->head_dim == 64 || cfg->head_dim == 128, FFMI_ERR_UNSUPPORTED);
+  FFMI_CHECK(cfg->num_heads > 0 && cfg->max_requests > 0 && cfg->max_seq_len > 0 &&
+                 cfg->max_tokens > 0,
+             FFMI_ERR_INVALID);
+  ffmi_attn *h = new ffmi_attn();
+  h->cfg = *cfg;
+  h->slots = (cfg->max_seq_len + cfg->max_tree_tokens + 31) & ~31;
+  const size_t Hl = (size_t)cfg->num_heads * cfg->head_dim;
+  const size_t kv = (size_t)cfg->max_requests * cfg->num_heads * h->slots * cfg->head_dim;
+  bool ok = hipMalloc((void **)&h->kc, kv * 2) == hipSuccess &&
+            hipMalloc((void **)&h->vc, kv * 2) == hipSuccess &&
+            hipMalloc((void **)&h->qbuf, (size_t)cfg->max_tokens * Hl * 2) == hipSuccess;
+  if (ok && cfg->mode == FFMI_ATTN_TREE)
+    ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * 2) == hipSuccess;
+  std::vector<float> tab;
+  rope_table(tab, h->slots, cfg->head_dim, cfg->rope_theta);
+  if (ok) ok = hipMalloc((void **)&h->rope, tab.size() * sizeof(float)) == hipSuccess;
+  if (!ok) {
+    ffmi_attn_destroy(h);
+    ffmi_set_last_error("attention cache alloc", __FILE__, __LINE__);
+    return FFMI_ERR_OOM;
+  }
+  // zero the caches: masked keys are multiplied by exactly-zero weights, so
+  // never-written slots must hold finite values
+  FFMI_HIP(hipMemset(h->kc, 0, kv * 2));
+  FFMI_HIP(hipMemset(h->vc, 0, kv * 2));
+  if (h->stage) FFMI_HIP(hipMemset(h->stage, 0, (size_t)cfg->max_tokens * 2 * Hl * 2));
+  FFMI_HIP(hipMemcpy(h->rope, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
+  *out = h;
+  return FFMI_OK;
+}
+
+extern "C" void ffmi_attn_destroy(ffmi_attn *h) {
+  if (!h) return;
+  (void)hipFree(h->kc);
+  (void)hipFree(h->vc);
+  (void)hipFree(h->qbuf);
+  (void)hipFree(h->stage);
+  (void)hipFree(h->rope);
+  delete h;
+}
+
+extern "C" ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *slots) {
+  FFMI_CHECK(h, FFMI_ERR_INVALID);
+  if (k) *k = h->kc;
+  if (v) *v = h->vc;
+  if (slots) *slots = h->slots;
+  return FFMI_OK;
+}
+
+static ffmi_status attn_run(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, void *out,
+                            ffmi_stream stream, bool tree) {
+  FFMI_CHECK(h && b && qkv && out, FFMI_ERR_INVALID);
+  FFMI_CHECK(b->num_tokens <= h->cfg.max_tokens, FFMI_ERR_INVALID);
+  const hipStream_t s = (hipStream_t)stream;
+  const int heads = h->cfg.num_heads, d = h->cfg.head_dim;
+  if (tree && b->num_commits > 0)
+    FFMI_HIP(ffmi::launch_commit(b->dev, b->num_commits, h->stage, h->kc, h->vc, heads, d,
+                                 h->slots, s));
+  FFMI_HIP(ffmi::launch_rope_store(b->dev, b->num_tokens, (const uint16_t *)qkv, h->qbuf, h->kc,
+                                   h->vc, tree ? h->stage : nullptr, h->rope, heads, d, h->slots,
+                                   h->slots, s));
+  FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, h->qbuf, h->kc, h->vc, (uint16_t *)out,
+                                  heads, d, h->slots, h->cfg.qk_scale, s));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_attn_inc(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                                     void *out, ffmi_stream stream) {
+  return attn_run(h, b, qkv, out, stream, false);
+}
+extern "C" ffmi_status ffmi_attn_spec(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                                      void *out, ffmi_stream stream) {
+  return attn_run(h, b, qkv, out, stream, false);
+}
+extern "C" ffmi_status ffmi_attn_tree(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                                      void *out, ffmi_stream stream) {
+  FFMI_CHECK(h && h->stage, FFMI_ERR_INVALID);  // created with FFMI_ATTN_TREE
+  return attn_run(h, b, qkv, out, stream, true);
+}
+
+// ---------------------------------------------------------------------------
+// linear / norms / aux
+// ---------------------------------------------------------------------------
+extern "C" size_t ffmi_linear_packed_bytes(int out_dim, int in_dim) {
+  const size_t nt = (size_t)(out_dim + 15) / 16, kt = (size_t)(in_dim + 31) / 32;
+  return nt * kt * 512 * 2;
+}
+
+extern "C" ffmi_status ffmi_linear_pack_weight(const void *W, int out_dim, int in_dim,
+                                               void *W_packed, ffmi_stream stream) {
+  FFMI_CHECK(W && W_packed && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)W, in_dim, 0, 0, out_dim, in_dim,
+                                    (uint16_t *)W_packed, 0, 0, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, int out_dim,
+                                                int in_dim, void *W_packed, ffmi_stream stream) {
+  FFMI_CHECK(Wg && Wu && W_packed && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)Wg, in_dim, 0, 0, out_dim, in_dim,
+                                    (uint16_t *)W_packed, 1, 0, (hipStream_t)stream));
+  FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)Wu, in_dim, 0, 0, out_dim, in_dim,
+                                    (uint16_t *)W_packed, 1, 1, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
+                                   int out_dim, int in_dim, int epilogue, ffmi_stream stream) {
+  FFMI_CHECK(X && W_packed && Y && T >= 0 && out_dim > 0, FFMI_ERR_INVALID);
+  FFMI_CHECK(in_dim > 0 && in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
+  FFMI_CHECK(epilogue == FFMI_EPI_NONE || epilogue == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_gemm((const uint16_t *)X, (const uint16_t *)W_packed, (uint16_t *)Y, T,
+                             out_dim, in_dim, epilogue, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rmsnorm(const void *x, const void *w, void *out, int T, int H,
+                                    float eps, ffmi_stream stream) {
+  FFMI_CHECK(x && w && out && H % 8 == 0 && H <= 16384, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_rmsnorm((const uint16_t *)x, nullptr, (const uint16_t *)w, nullptr,
+                                (uint16_t *)out, T, H, eps, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_residual_rmsnorm(const void *x1, const void *x2, const void *w,
+                                             void *residual_out, void *out, int T, int H,
+                                             float eps, ffmi_stream stream) {
+  FFMI_CHECK(x1 && x2 && w && residual_out && out && H % 8 == 0 && H <= 16384, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_rmsnorm((const uint16_t *)x1, (const uint16_t *)x2, (const uint16_t *)w,
+                                (uint16_t *)residual_out, (uint16_t *)out, T, H, eps,
+                                (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_embedding(const ffmi_batch_dev *b, const void *table, void *out,
+                                      int H, ffmi_stream stream) {
+  FFMI_CHECK(b && table && out && H % 8 == 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_embedding(b->dev, b->num_tokens, (const uint16_t *)table,
+                                  (uint16_t *)out, H, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_silu_mul(const void *a, const void *b, void *out, size_t n,
+                                     ffmi_stream stream) {
+  FFMI_CHECK(a && b && out, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_silu_mul((const uint16_t *)a, (const uint16_t *)b, (uint16_t *)out, n,
+                                 (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_argmax(const void *logits, int T, int V, int32_t *ids, float *probs,
+                                   ffmi_stream stream) {
+  FFMI_CHECK(logits && ids && V > 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_argmax((const uint16_t *)logits, T, V, 1, ids, probs,
+                               (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, int32_t *ids,
+                                     float *probs, ffmi_stream stream) {
+  FFMI_CHECK(logits && ids && V > 0 && k >= 1 && k <= 4 && k <= V, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_argmax((const uint16_t *)logits, T, V, k, ids, probs,
+                               (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *name, uint64_t seed,
+                                        int kind, ffmi_stream stream) {
+  FFMI_CHECK(dst_f16 && name, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_fill_weight((uint16_t *)dst_f16, n, ffmi::weight_key(name, seed), kind,
+                                    (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+// ---------------------------------------------------------------------------
+// RCCL all-reduce (RCCL over xGMI; the reference: ncclAllReduce,
+// allreduce_kernels.cu:67-74)
+// ---------------------------------------------------------------------------
+struct ffmi_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0;
+};
+
+extern "C" ffmi_status ffmi_comm_unique_id(void *id_out) {
+  FFMI_CHECK(id_out, FFMI_ERR_INVALID);
+  static_assert(sizeof(ncclUniqueId) == FFMI_UNIQUE_ID_BYTES, "unique id size");
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) return FFMI_ERR_NCCL;
+  memcpy(id_out, &id, sizeof(id));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_comm_create(const void *id, int nranks, int rank, ffmi_comm **out) {
+  FFMI_CHECK(id && out && nranks >= 1 && rank >= 0 && rank < nranks, FFMI_ERR_INVALID);
+  ffmi_comm *c = new ffmi_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, uid, rank);
+  if (r != ncclSuccess) {
+    ffmi_set_last_error(ncclGetErrorString(r), __FILE__, __LINE__);
+    delete c;
+    return FFMI_ERR_NCCL;
+  }
+  *out = c;
+  return FFMI_OK;
+}
+
+extern "C" void ffmi_comm_destroy(ffmi_comm *c) {
+  if (!c) return;
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+}
+
+extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
+                                      int dtype, ffmi_stream stream) {
+  FFMI_CHECK(c && in && out, FFMI_ERR_INVALID);
+  if (c->nranks == 1) {
+    if (in != out) {
+      const size_t esz = dtype == FFMI_F16 ? 2 : 4;
+      FFMI_HIP(hipMemcpyAsync(out, in, count * esz, hipMemcpyDeviceToDevice, (hipStream_t)stream));
+    }
+    return FFMI_OK;
+  }
+  ncclDataType_t t = dtype == FFMI_F16 ? ncclHalf : (dtype == FFMI_F32 ? ncclFloat : ncclInt32);
+  ncclResult_t r = ncclAllReduce(in, out, count, t, ncclSum, c->comm, (hipStream_t)stream);
+  if (r != ncclSuccess) {
+    ffmi_set_last_error(ncclGetErrorString(r), __FILE__, __LINE__);
+    return FFMI_ERR_NCCL;
+  }
+  return FFMI_OK;
+}

@@ -1,0 +1,99 @@
+// ffmi_internal.h -- shared internals of libffmi.so (gfx950 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+#include <stdint.h>
+
+#include "../../include/ffmi.h"
+
+#define FFMI_HIP(expr)                                   \
+  do {                                                   \
+    hipError_t e_ = (expr);                              \
+    if (e_ != hipSuccess) {                              \
+      ffmi_set_last_error(hipGetErrorString(e_), __FILE__, __LINE__); \
+      return FFMI_ERR_HIP;                               \
+    }                                                    \
+  } while (0)
+
+#define FFMI_CHECK(cond, code)                                         \
+  do {                                                                 \
+    if (!(cond)) {                                                     \
+      ffmi_set_last_error(#cond, __FILE__, __LINE__);                  \
+      return (code);                                                   \
+    }                                                                  \
+  } while (0)
+
+void ffmi_set_last_error(const char *msg, const char *file, int line);
+
+namespace ffmi {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+// Layout of the packed per-step metadata blob (device copy of ffmi_batch_desc).
+struct BatchHeader {
+  int32_t num_tokens, num_work, num_commits, num_mask_reqs;
+  int32_t off_tokens, off_work, off_commits, off_masks;  // byte offsets
+};
+
+struct BatchView {
+  const BatchHeader *hdr;
+  const ffmi_token_info *tokens;
+  const ffmi_attn_work *work;
+  const ffmi_commit_info *commits;
+  const uint64_t *masks;
+};
+
+__device__ __forceinline__ BatchView batch_view(const char *blob) {
+  BatchView v;
+  v.hdr = reinterpret_cast<const BatchHeader *>(blob);
+  v.tokens = reinterpret_cast<const ffmi_token_info *>(blob + v.hdr->off_tokens);
+  v.work = reinterpret_cast<const ffmi_attn_work *>(blob + v.hdr->off_work);
+  v.commits = reinterpret_cast<const ffmi_commit_info *>(blob + v.hdr->off_commits);
+  v.masks = reinterpret_cast<const uint64_t *>(blob + v.hdr->off_masks);
+  return v;
+}
+
+// ---- kernel launchers (defined in kernels/*.hip) ----
+hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
+                              hipStream_t s);
+hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
+                              int N, int K, uint16_t *dst, int interleave_gate_up,
+                              int tile_offset, hipStream_t s);
+hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T,
+                       int N, int K, int epilogue, hipStream_t s);
+hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
+                          uint16_t *res_out, uint16_t *out, int T, int H, float eps,
+                          hipStream_t s);
+hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
+                            uint16_t *out, int H, hipStream_t s);
+hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
+                           size_t n, hipStream_t s);
+hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
+                         float *probs, hipStream_t s);
+hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv,
+                             uint16_t *qbuf, uint16_t *kc, uint16_t *vc,
+                             uint16_t *stage, const float *rope, int heads, int d,
+                             int slots, int max_rope_pos, hipStream_t s);
+hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
+                         uint16_t *kc, uint16_t *vc, int heads, int d, int slots,
+                         hipStream_t s);
+hipError_t launch_attention(const char *blob, int W, const uint16_t *qbuf,
+                            const uint16_t *kc, const uint16_t *vc, uint16_t *out,
+                            int heads, int d, int slots, float scale, hipStream_t s);
+
+uint64_t weight_key(const char *name, uint64_t seed);
+
+}  // namespace ffmi
+
+// Device batch blob: pinned host staging + device copy.
+struct ffmi_batch_dev {
+  char *host = nullptr;  // pinned
+  char *dev = nullptr;
+  size_t cap = 0;
+  int max_tokens = 0, max_requests = 0;
+  // host-visible counts of the last upload (launch geometry)
+  int num_tokens = 0, num_work = 0, num_commits = 0, num_mask_reqs = 0;
+  hipEvent_t uploaded = nullptr;  // guards reuse of the pinned staging
+};

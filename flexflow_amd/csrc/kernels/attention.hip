@@ -1,0 +1,299 @@
+// attention.hip -- incremental / speculative / tree-verify attention on MFMA.
+//
+// One kernel family serves the reference's three attention ops, because on
+// the device they differ only in WHICH cache slots a query may see:
+//  * IncMultiHeadSelfAttention    (inc_multihead_self_attention.cu:372-623,
+//    prompt path :98-366): keys [0, pos] (causal);
+//  * TreeIncMultiHeadSelfAttention (tree_inc_multihead_self_attention.cu:
+//    35-333): keys [0, non_tree_cache_size) plus tree slot j iff
+//    causalMask.mask[j] has the query's bit (layer-order token tree);
+//  * SpecIncMultiHeadSelfAttention (spec_inc_multihead_self_attention.cu:
+//    36-309): same bitmask rule with the query's tree index as its bit.
+// The host packs that rule per token (ffmi_token_info: prefix_len,
+// tree_base/len/bit), so the kernel is mode-agnostic.  (The reference's
+// `1 << qi` on a 32-bit int, tree_inc...cu:168-169, is done in 64 bits here.)
+//
+// KV-cache layout (handle-owned, MI355X-first): K[req][head][slot][d] and
+// V^T[req][head][d][slot], slots = S + tree rounded up to 32.  With these two
+// orientations both attention GEMMs read their MFMA operands straight from
+// HBM as 16-B / 8-B vectors:
+//   S^T[key][q] = K . Q^T        (A = K rows, B = Q rows)   16x16x32 f16
+//   O^T[d][q]  += V^T . P^T      (A = V^T rows, B = P^T)    16x16x32 f16
+// and the S^T accumulator of a lane (query q = lane&15, keys 4g..4g+3 of
+// each 16-key half, g = lane>>4) IS the lane's P^T B-fragment under the key
+// permutation k(g,j) = (j<4 ? 4g+j : 16+4g+j-4) -- no LDS transpose.  P is
+// fed as an fp16 hi/lo pair (two MFMAs), which keeps ~22 bits of P, matching
+// the reference's fp32 P.V accumulation (inc...cu:575-581) instead of
+// rounding P to fp16.  Softmax follows the reference: __expf, running max,
+// out = sum(e_j v_j) / (sum_j e_j + 1e-6)   (inc...cu:532-547).
+//
+// Work decomposition: one workgroup per (work item = <=16 queries of one
+// request, head); its 4 waves stride over 32-key chunks with private online
+// softmax state and merge through LDS.  Every key/value byte of a request is
+// read once per 16-query tile (the reference's tree kernel re-reads the
+// whole K/V once per query, tree_inc...cu:135).
+#include "../ffmi_internal.h"
+
+namespace ffmi {
+
+__device__ __forceinline__ float h2f(uint16_t v) { return __half2float(__ushort_as_half(v)); }
+__device__ __forceinline__ uint16_t f2h(float v) { return __half_as_ushort(__float2half_rn(v)); }
+
+// RoPE (HF rotate-half, inc...cu:664-738) + KV store (store_kv_cache
+// inc...cu:35-61 / update_tree_branch_kv_cache_fused tree_inc...cu:433-478 /
+// spec_inc_store_kv_cache spec_inc...cu:311-358) + staging copy for commits.
+__global__ void rope_store_kernel(const char *__restrict__ blob, int T,
+                                  const uint16_t *__restrict__ qkv,
+                                  uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
+                                  uint16_t *__restrict__ vc, uint16_t *__restrict__ stage,
+                                  const float *__restrict__ rope, int heads, int d,
+                                  int slots, int max_rope_pos) {
+  const int hd = d >> 1;
+  const int ppb = blockDim.x / hd;
+  const int pair = blockIdx.x * ppb + threadIdx.x / hd;
+  const int i = threadIdx.x % hd;
+  if (pair >= T * heads) return;
+  const int t = pair / heads, h = pair % heads;
+  BatchView bv = batch_view(blob);
+  const ffmi_token_info ti = bv.tokens[t];
+  const int Hl = heads * d;
+  const uint16_t *qrow = qkv + (size_t)t * 3 * Hl + h * d;
+  const uint16_t *krow = qrow + Hl;
+  const uint16_t *vrow = qrow + 2 * Hl;
+  const int pos = min(max(ti.pos, 0), max_rope_pos - 1);
+  const float c = rope[((size_t)pos * hd + i) * 2 + 0];
+  const float s = rope[((size_t)pos * hd + i) * 2 + 1];
+  float a = h2f(qrow[i]), b = h2f(qrow[i + hd]);
+  const uint16_t q0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
+  const uint16_t q1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
+  a = h2f(krow[i]);
+  b = h2f(krow[i + hd]);
+  const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
+  const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
+  const uint16_t v0 = vrow[i], v1 = vrow[i + hd];
+  uint16_t *qo = qbuf + (size_t)t * Hl + h * d;
+  qo[i] = q0;
+  qo[i + hd] = q1;
+  if (ti.store_slot >= 0 && ti.store_slot < slots) {
+    uint16_t *kr = kc + (((size_t)ti.req * heads + h) * slots + ti.store_slot) * d;
+    kr[i] = k0;
+    kr[i + hd] = k1;
+    uint16_t *vt = vc + ((size_t)ti.req * heads + h) * d * slots + ti.store_slot;
+    vt[(size_t)i * slots] = v0;
+    vt[(size_t)(i + hd) * slots] = v1;
+  }
+  if (stage) {
+    uint16_t *st = stage + (size_t)t * 2 * Hl + h * d;
+    st[i] = k0;
+    st[i + hd] = k1;
+    st[Hl + i] = v0;
+    st[Hl + i + hd] = v1;
+  }
+}
+
+hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv, uint16_t *qbuf,
+                             uint16_t *kc, uint16_t *vc, uint16_t *stage, const float *rope,
+                             int heads, int d, int slots, int max_rope_pos, hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  const int hd = d / 2;
+  const int ppb = 256 / hd;
+  const int pairs = T * heads;
+  hipLaunchKernelGGL(rope_store_kernel, dim3((pairs + ppb - 1) / ppb), dim3(ppb * hd), 0, s,
+                     blob, T, qkv, qbuf, kc, vc, stage, rope, heads, d, slots, max_rope_pos);
+  return hipGetLastError();
+}
+
+// commit_tokens_kernel (tree_inc...cu:335-396): accepted tokens of the
+// previous verify batch move from the staging rows to their depth slot.
+__global__ void commit_kernel(const char *__restrict__ blob, int C,
+                              const uint16_t *__restrict__ stage, uint16_t *__restrict__ kc,
+                              uint16_t *__restrict__ vc, int heads, int d, int slots) {
+  const int item = blockIdx.x;  // commit * heads + head
+  const int ci = item / heads, h = item % heads;
+  if (ci >= C) return;
+  BatchView bv = batch_view(blob);
+  const ffmi_commit_info cm = bv.commits[ci];
+  if (cm.depth < 0 || cm.depth >= slots) return;
+  const int Hl = heads * d;
+  const uint16_t *st = stage + (size_t)cm.src_token * 2 * Hl + h * d;
+  for (int i = threadIdx.x; i < d; i += blockDim.x) {
+    kc[(((size_t)cm.req * heads + h) * slots + cm.depth) * d + i] = st[i];
+    vc[(((size_t)cm.req * heads + h) * d + i) * slots + cm.depth] = st[Hl + i];
+  }
+}
+
+hipError_t launch_commit(const char *blob, int C, const uint16_t *stage, uint16_t *kc,
+                         uint16_t *vc, int heads, int d, int slots, hipStream_t s) {
+  if (C <= 0) return hipSuccess;
+  hipLaunchKernelGGL(commit_kernel, dim3(C * heads), dim3(64), 0, s, blob, C, stage, kc, vc,
+                     heads, d, slots);
+  return hipGetLastError();
+}
+
+__device__ __forceinline__ bool key_visible(int slot, const ffmi_token_info &ti,
+                                            const uint64_t *mask) {
+  if (slot < ti.prefix_len) return true;
+  const unsigned j = (unsigned)(slot - ti.tree_base);
+  if (j < (unsigned)ti.tree_len) return (mask[j] >> ti.tree_bit) & 1ull;
+  return false;
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void attention_kernel(
+    const char *__restrict__ blob, const uint16_t *__restrict__ qbuf,
+    const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
+    uint16_t *__restrict__ out, int heads, int slots, float scale) {
+  constexpr int KS = D / 32;  // k-steps of the QK^T product
+  constexpr int DT = D / 16;  // d-tiles of the PV product
+  __shared__ float sm_m[4][16];
+  __shared__ float sm_l[4][16];
+  __shared__ __attribute__((aligned(16))) float sm_o[4][DT][4][64];
+
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int qi = lane & 15;
+  const int g = lane >> 4;
+  const int h = blockIdx.y;
+  const BatchView bv = batch_view(blob);
+  const ffmi_attn_work w = bv.work[blockIdx.x];
+  const int Hl = heads * D;
+  const bool qvalid = qi < w.q_count;
+  const ffmi_token_info ti = bv.tokens[w.q_start + (qvalid ? qi : 0)];
+  const uint64_t *mask = bv.masks + (size_t)w.req * FFMI_MAX_TREE;
+
+  h8 qf[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    if (qvalid)
+      qf[ks] = *reinterpret_cast<const h8 *>(qbuf + (size_t)(w.q_start + qi) * Hl + h * D +
+                                             32 * ks + 8 * g);
+    else
+      qf[ks] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+  }
+  const uint16_t *kbase = kc + ((size_t)w.req * heads + h) * slots * D;
+  const uint16_t *vbase = vc + ((size_t)w.req * heads + h) * D * slots;
+
+  const float NEG = -INFINITY;
+  float m_run = NEG, l_run = 0.f;
+  f4 o[DT];
+#pragma unroll
+  for (int t = 0; t < DT; ++t) o[t] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int nchunks = (w.kv_len + 31) >> 5;
+  for (int c = wave; c < nchunks; c += 4) {
+    const int base = c * 32;
+    f4 s[2];
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      s[sub] = f4{0.f, 0.f, 0.f, 0.f};
+      const uint16_t *krow = kbase + (size_t)(base + sub * 16 + (lane & 15)) * D + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        h8 a = *reinterpret_cast<const h8 *>(krow + 32 * ks);
+        s[sub] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, qf[ks], s[sub], 0, 0, 0);
+      }
+    }
+    // V^T fragments for this chunk (issued early; consumed after softmax)
+    h8 va[DT];
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t *vrow = vbase + (size_t)(t * 16 + (lane & 15)) * slots + base + 4 * g;
+      h4 v0 = *reinterpret_cast<const h4 *>(vrow);
+      h4 v1 = *reinterpret_cast<const h4 *>(vrow + 16);
+      va[t] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+    float sc[8];
+    bool vis[8];
+    float cmax = NEG;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int slot = base + (j >> 2) * 16 + 4 * g + (j & 3);
+      vis[j] = qvalid && slot < w.kv_len && key_visible(slot, ti, mask);
+      sc[j] = __fmul_rn(scale, s[j >> 2][j & 3]);
+      cmax = vis[j] ? fmaxf(cmax, sc[j]) : cmax;
+    }
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32));
+    const float m_new = fmaxf(m_run, cmax);
+    const float m_use = (m_new == NEG) ? 0.f : m_new;
+    const float alpha = (m_run == NEG) ? 0.f : __expf(m_run - m_use);
+    h8 phi, plo;
+    float psum = 0.f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float e = vis[j] ? __expf(sc[j] - m_use) : 0.f;
+      psum += e;
+      const _Float16 hi = (_Float16)e;
+      phi[j] = hi;
+      plo[j] = (_Float16)(e - (float)hi);
+    }
+    l_run = l_run * alpha + psum;
+    m_run = m_new;
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      o[t] *= alpha;
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[t], phi, o[t], 0, 0, 0);
+      o[t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[t], plo, o[t], 0, 0, 0);
+    }
+  }
+
+  // per-query partial sum over the 4 lane groups (same m_run in all four)
+  l_run += __shfl_xor(l_run, 16);
+  l_run += __shfl_xor(l_run, 32);
+  if (g == 0) {
+    sm_m[wave][qi] = m_run;
+    sm_l[wave][qi] = l_run;
+  }
+#pragma unroll
+  for (int t = 0; t < DT; ++t)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sm_o[wave][t][r][lane] = o[t][r];
+  __syncthreads();
+
+  // merge: wave w finalizes d-tiles t = w, w+4, ...
+  float M = NEG;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_m[ww][qi]);
+  float f[4], L = 0.f;
+#pragma unroll
+  for (int ww = 0; ww < 4; ++ww) {
+    const float mw = sm_m[ww][qi];
+    f[ww] = (mw == NEG) ? 0.f : __expf(mw - M);
+    L += f[ww] * sm_l[ww][qi];
+  }
+  const float inv = 1.0f / (L + 1e-6f);
+  if (!qvalid) return;
+  uint16_t *orow = out + (size_t)(w.q_start + qi) * Hl + h * D;
+  for (int t = wave; t < DT; t += 4) {
+    uint16_t r4[4];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float acc = 0.f;
+#pragma unroll
+      for (int ww = 0; ww < 4; ++ww) acc += f[ww] * sm_o[ww][t][r][lane];
+      r4[r] = f2h(acc * inv);
+    }
+    uint2 pk;
+    pk.x = r4[0] | ((uint32_t)r4[1] << 16);
+    pk.y = r4[2] | ((uint32_t)r4[3] << 16);
+    *reinterpret_cast<uint2 *>(orow + t * 16 + 4 * g) = pk;
+  }
+}
+
+hipError_t launch_attention(const char *blob, int W, const uint16_t *qbuf, const uint16_t *kc,
+                            const uint16_t *vc, uint16_t *out, int heads, int d, int slots,
+                            float scale, hipStream_t s) {
+  if (W <= 0) return hipSuccess;
+  dim3 grid(W, heads);
+  if (d == 128)
+    hipLaunchKernelGGL(attention_kernel<128>, grid, dim3(256), 0, s, blob, qbuf, kc, vc, out,
+                       heads, slots, scale);
+  else if (d == 64)
+    hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(256), 0, s, blob, qbuf, kc, vc, out,
+                       heads, slots, scale);
+  else
+    return hipErrorInvalidValue;
+  return hipGetLastError();
+}
+
+}  // namespace ffmi

@@ -1,0 +1,213 @@
+// norm.hip -- RMSNorm / ResidualRMSNorm, embedding, SiLU-mul, softmax+argmax/topk.
+//
+// HBM-bound row kernels: one 256-thread workgroup per row, 16-B vector
+// loads/stores (8 halves per lane), the row kept in registers between the
+// reduction and the scale pass (one read + one write per element).  Unlike
+// the reference (which launches every buffer row, rms_norm_kernels.cu:133-134)
+// only the T active rows are processed.
+#include "../ffmi_internal.h"
+
+namespace ffmi {
+
+__device__ __forceinline__ float h2f_(uint16_t v) { return __half2float(__ushort_as_half(v)); }
+__device__ __forceinline__ uint16_t f2h_(float v) { return __half_as_ushort(__float2half_rn(v)); }
+
+template <typename T>
+__device__ __forceinline__ T block_sum256(T v, T *scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) scratch[wave] = v;
+  __syncthreads();
+  T r = (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
+  __syncthreads();
+  return r;
+}
+
+// rms_norm_kernels.cu:97-124 / residual_rms_norm_kernels.cu:98-131:
+//   r = x1 (+ x2, rounded to half); rms = half(rsqrt(mean(r^2) + eps));
+//   y = half(r * rms); out = half(y * w)
+template <int MAXC>
+__global__ __launch_bounds__(256) void rmsnorm_kernel(
+    const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
+    const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
+    uint16_t *__restrict__ out, int H, float eps) {
+  __shared__ float scratch[4];
+  const int row = blockIdx.x;
+  const int nchunk = H >> 3;
+  const uint16_t *a = x1 + (size_t)row * H;
+  const uint16_t *b = x2 ? x2 + (size_t)row * H : nullptr;
+  uint4 v[MAXC];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = threadIdx.x + c * 256;
+    if (ch < nchunk) {
+      uint4 xa = *reinterpret_cast<const uint4 *>(a + ch * 8);
+      if (b) {
+        uint4 xb = *reinterpret_cast<const uint4 *>(b + ch * 8);
+        const __half2 *pa = reinterpret_cast<const __half2 *>(&xa);
+        const __half2 *pb = reinterpret_cast<const __half2 *>(&xb);
+        __half2 r[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) r[q] = __hadd2(pa[q], pb[q]);  // correctly rounded
+        xa = *reinterpret_cast<uint4 *>(r);
+        *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
+      }
+      v[c] = xa;
+      const uint16_t *e = reinterpret_cast<const uint16_t *>(&xa);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float f = h2f_(e[q]);
+        ss += f * f;
+      }
+    }
+  }
+  const float sum = block_sum256(ss, scratch);
+  const float rms_f = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
+  const float rms = h2f_(f2h_(rms_f));
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = threadIdx.x + c * 256;
+    if (ch < nchunk) {
+      uint4 wv = *reinterpret_cast<const uint4 *>(w + ch * 8);
+      const uint16_t *e = reinterpret_cast<const uint16_t *>(&v[c]);
+      const uint16_t *we = reinterpret_cast<const uint16_t *>(&wv);
+      uint16_t o8[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float y = h2f_(f2h_(__fmul_rn(h2f_(e[q]), rms)));
+        o8[q] = f2h_(__fmul_rn(y, h2f_(we[q])));
+      }
+      *reinterpret_cast<uint4 *>(out + (size_t)row * H + ch * 8) =
+          *reinterpret_cast<uint4 *>(o8);
+    }
+  }
+}
+
+hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
+                          uint16_t *res_out, uint16_t *out, int T, int H, float eps,
+                          hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  if (H % 8 != 0 || H > 8 * 256 * 8) return hipErrorInvalidValue;
+  const int nchunk = H / 8;
+  if (nchunk <= 256)
+    hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
+                       H, eps);
+  else if (nchunk <= 512)
+    hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
+                       H, eps);
+  else if (nchunk <= 1024)
+    hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
+                       H, eps);
+  else
+    hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
+                       H, eps);
+  return hipGetLastError();
+}
+
+// embed_forward_no_aggr (embedding_kernels.cu:233-244)
+__global__ void embedding_kernel(const char *__restrict__ blob,
+                                 const uint16_t *__restrict__ table,
+                                 uint16_t *__restrict__ out, int H) {
+  const BatchView bv = batch_view(blob);
+  const int t = blockIdx.x;
+  const int tok = bv.tokens[t].token_id;
+  const uint4 *src = reinterpret_cast<const uint4 *>(table + (size_t)tok * H);
+  uint4 *dst = reinterpret_cast<uint4 *>(out + (size_t)t * H);
+  for (int c = threadIdx.x; c < H / 8; c += blockDim.x) dst[c] = src[c];
+}
+
+hipError_t launch_embedding(const char *blob, int T, const uint16_t *table, uint16_t *out,
+                            int H, hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  if (H % 8 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(embedding_kernel, dim3(T), dim3(256), 0, s, blob, table, out, H);
+  return hipGetLastError();
+}
+
+// SigmoidSiluMultiKernel (sigmoid_silu_multi.cu:37-47)
+__global__ void silu_mul_kernel(const uint16_t *__restrict__ a, const uint16_t *__restrict__ b,
+                                uint16_t *__restrict__ out, size_t n) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    const float g = h2f_(a[i]);
+    const float sg = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-g)));
+    const float t = h2f_(f2h_(__fmul_rn(g, h2f_(f2h_(sg)))));
+    out[i] = f2h_(__fmul_rn(t, h2f_(b[i])));
+  }
+}
+
+hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out, size_t n,
+                           hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 16384) blocks = 16384;
+  hipLaunchKernelGGL(silu_mul_kernel, dim3((unsigned)blocks), dim3(256), 0, s, a, b, out, n);
+  return hipGetLastError();
+}
+
+// softmax (fp16 output, softmax.cu:262-288) + ArgMax (argmax.cu:62-100) /
+// ArgTopK (arg_topk.cu:339-448).  p_i = half(exp(x_i - max) / sum); the
+// greedy pick is the lowest index of the largest p_i (ties created by the
+// fp16 rounding resolve exactly as cub ArgMax / the top-k heap do).  k
+// rounds of a block-wide (p desc, idx asc) selection.
+__global__ __launch_bounds__(256) void softmax_topk_kernel(
+    const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
+    float *__restrict__ probs) {
+  __shared__ float fscratch[4];
+  __shared__ unsigned long long kscratch[4];
+  const int row = blockIdx.x;
+  const uint16_t *x = logits + (size_t)row * V;
+  float mx = -INFINITY;
+  for (int i = threadIdx.x; i < V; i += 256) mx = fmaxf(mx, h2f_(x[i]));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if ((threadIdx.x & 63) == 0) fscratch[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = fmaxf(fmaxf(fscratch[0], fscratch[1]), fmaxf(fscratch[2], fscratch[3]));
+  __syncthreads();
+  float se = 0.f;
+  for (int i = threadIdx.x; i < V; i += 256) se += expf(h2f_(x[i]) - mx);
+  const float sum = block_sum256(se, fscratch);
+  int chosen[4] = {-1, -1, -1, -1};
+  for (int r = 0; r < k; ++r) {
+    // key = (p bits << 32) | (~idx): max key = largest p, lowest index
+    unsigned long long best = 0;
+    for (int i = threadIdx.x; i < V; i += 256) {
+      bool taken = false;
+      for (int q = 0; q < r; ++q) taken |= (chosen[q] == i);
+      if (taken) continue;
+      const uint16_t p = f2h_(__fdiv_rn(expf(h2f_(x[i]) - mx), sum));
+      const unsigned long long key =
+          ((unsigned long long)p << 32) | (unsigned long long)(0xffffffffu - (unsigned)i);
+      best = key > best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      unsigned long long other = __shfl_xor(best, o);
+      best = other > best ? other : best;
+    }
+    if ((threadIdx.x & 63) == 0) kscratch[threadIdx.x >> 6] = best;
+    __syncthreads();
+    unsigned long long b = kscratch[0];
+    for (int q = 1; q < 4; ++q) b = kscratch[q] > b ? kscratch[q] : b;
+    __syncthreads();
+    const int idx = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    chosen[r] = idx;
+    if (threadIdx.x == 0) {
+      ids[(size_t)row * k + r] = idx;
+      if (probs) probs[(size_t)row * k + r] = h2f_((uint16_t)(b >> 32));
+    }
+  }
+}
+
+hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
+                         float *probs, hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  if (k < 1 || k > 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
+  return hipGetLastError();
+}
+
+}  // namespace ffmi

@@ -1,0 +1,94 @@
+// weights.hip -- seeded synthetic weights and MFMA-fragment weight packing.
+//
+// Weight values follow the counter-based splitmix64 spec of
+// oracle/oracle.h:orc_gen_weight bit for bit (no FMA contraction: explicit
+// _rn intrinsics), so the GPU model and the CPU oracle hold identical fp16
+// weights without shipping checkpoints (none exist offline).
+//
+// Packed layout ("MFMA B-fragment order") for Y = X . W^T with
+// v_mfma_f32_16x16x32_f16: the [N][K] matrix is cut into 16x32 blocks; block
+// (nt, kt) is 1 KiB at ((nt * KT) + kt) * 512 halves, and lane l of a wave
+// owns halves [l*8, l*8+8) = W[nt*16 + (l&15)][kt*32 + 8*(l>>4) + 0..7],
+// exactly the B operand the MFMA wants.  A wave streaming one N-tile reads
+// contiguous 1 KiB per k-step (fully coalesced, 16 B/lane).
+#include "../ffmi_internal.h"
+
+namespace ffmi {
+
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, int kind) {
+  const float center = kind == 1 ? 1.0f : 0.0f;
+  const float amp = kind == 1 ? 0.1f : 0.034641016f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
+       i += (size_t)gridDim.x * blockDim.x) {
+    uint64_t x = splitmix64(key + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+    float t = __fsub_rn(__fmul_rn(2.0f, u), 1.0f);
+    float w = __fadd_rn(center, __fmul_rn(t, amp));
+    dst[i] = __half_as_ushort(__float2half_rn(w));
+  }
+}
+
+hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
+                              hipStream_t s) {
+  if (n == 0) return hipSuccess;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(fill_weight_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, n,
+                     key, kind);
+  return hipGetLastError();
+}
+
+uint64_t weight_key(const char *name, uint64_t seed) {
+  uint64_t h = 1469598103934665603ull;
+  for (const char *p = name; *p; ++p) {
+    h ^= (uint8_t)*p;
+    h *= 1099511628211ull;
+  }
+  return seed ^ h;
+}
+
+// One thread per (block, lane): gathers 8 halves of W[row][k..k+7].
+__global__ void pack_weight_kernel(const uint16_t *__restrict__ src, int ld, int row0,
+                                   int col0, int N, int K, int NT, int KT,
+                                   uint16_t *__restrict__ dst, int interleave,
+                                   int tile_offset) {
+  long gid = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  long total = (long)NT * KT * 64;
+  if (gid >= total) return;
+  int lane = (int)(gid & 63);
+  long blk = gid >> 6;
+  int kt = (int)(blk % KT);
+  int nt = (int)(blk / KT);
+  int n = nt * 16 + (lane & 15);
+  int k = kt * 32 + 8 * (lane >> 4);
+  uint16_t v[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = (n < N && k + j < K) ? src[(size_t)(row0 + n) * ld + col0 + k + j] : 0;
+  long dtile = interleave ? (2L * nt + tile_offset) : nt;
+  uint4 pk;
+  pk.x = v[0] | ((uint32_t)v[1] << 16);
+  pk.y = v[2] | ((uint32_t)v[3] << 16);
+  pk.z = v[4] | ((uint32_t)v[5] << 16);
+  pk.w = v[6] | ((uint32_t)v[7] << 16);
+  *reinterpret_cast<uint4 *>(dst + ((dtile * KT + kt) * 512 + lane * 8)) = pk;
+}
+
+hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0, int N,
+                              int K, uint16_t *dst, int interleave, int tile_offset,
+                              hipStream_t s) {
+  int NT = (N + 15) / 16, KT = (K + 31) / 32;
+  long total = (long)NT * KT * 64;
+  unsigned blocks = (unsigned)((total + 255) / 256);
+  hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, src, ld, row0,
+                     col0, N, K, NT, KT, dst, interleave, tile_offset);
+  return hipGetLastError();
+}
+
+}  // namespace ffmi

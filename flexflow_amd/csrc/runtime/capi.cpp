@@ -1,0 +1,130 @@
+// capi.cpp -- C ABI of the serving runtime (models + RequestManager).
+#include <vector>
+
+#include "request_manager.h"
+
+struct ffmi_rm {
+  ffmi::RequestManager rm;
+};
+
+extern "C" ffmi_status ffmi_model_create(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
+                                         ffmi_model **out) {
+  return ffmi::create_llama_gpu(cfg, o, out);
+}
+
+extern "C" void ffmi_model_destroy(ffmi_model *m) { delete m; }
+
+extern "C" ffmi_status ffmi_model_set_profiling(ffmi_model *m, int level) {
+  if (!m || level < 0 || level > 2) return FFMI_ERR_INVALID;
+  return m->set_profiling(level);
+}
+
+extern "C" int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap) {
+  if (!m) return -1;
+  return m->op_stats(out, cap);
+}
+
+extern "C" ffmi_status ffmi_set_device(int device) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FFMI_ERR_NO_DEVICE;
+  if (device < 0 || device >= n) return FFMI_ERR_INVALID;
+  return hipSetDevice(device) == hipSuccess ? FFMI_OK : FFMI_ERR_HIP;
+}
+
+extern "C" ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
+                                                   int max_seq, int max_tree, uint64_t salt,
+                                                   int disagree_pct, ffmi_model **out) {
+  if (!out) return FFMI_ERR_INVALID;
+  return ffmi::create_hash_model(vocab, mode, max_requests, max_seq, max_tree, salt,
+                                 disagree_pct, out);
+}
+
+extern "C" ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out) {
+  if (!cfg || !out) return FFMI_ERR_INVALID;
+  if (cfg->max_requests_per_batch <= 0 ||
+      cfg->max_requests_per_batch > ffmi::BatchConfig::MAX_NUM_REQUESTS ||
+      cfg->max_tokens_per_batch <= 0 || cfg->max_sequence_length <= 0 ||
+      cfg->max_spec_tree_token_num < 0 ||
+      cfg->max_spec_tree_token_num > ffmi::BatchConfig::MAX_SPEC_TREE_TOKEN_NUM)
+    return FFMI_ERR_INVALID;
+  if (cfg->max_tokens_per_batch + cfg->max_spec_tree_token_num * cfg->max_requests_per_batch >
+      ffmi::BatchConfig::MAX_NUM_TOKENS)
+    return FFMI_ERR_INVALID;
+  ffmi_rm *r = new ffmi_rm();
+  r->rm.set_max_requests_per_batch(cfg->max_requests_per_batch);
+  r->rm.set_max_tokens_per_batch(cfg->max_tokens_per_batch);
+  r->rm.set_max_spec_tree_token_num(cfg->max_spec_tree_token_num);
+  r->rm.set_max_sequence_length(cfg->max_sequence_length);
+  std::vector<int> eos;
+  for (int i = 0; i < cfg->num_eos; ++i) eos.push_back(cfg->eos_token_ids[i]);
+  r->rm.register_tokenizer(cfg->bos_token_id, eos);
+  for (int i = 0; i < cfg->num_tree_width; ++i)
+    if (!r->rm.push_spec_infer_tree_width(cfg->spec_tree_width[i])) {
+      delete r;
+      return FFMI_ERR_INVALID;  // tree_width <= MAX_BEAM_WIDTH (request_manager.cc:168-171)
+    }
+  r->rm.set_verbose(cfg->verbose != 0);
+  *out = r;
+  return FFMI_OK;
+}
+
+extern "C" void ffmi_rm_destroy(ffmi_rm *rm) { delete rm; }
+
+extern "C" ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm) {
+  if (!rm || !ssm || ssm->mode != FFMI_MODEL_BEAM) return FFMI_ERR_INVALID;
+  rm->rm.register_ssm_model(ssm);
+  return FFMI_OK;
+}
+
+extern "C" int64_t ffmi_rm_register_request(ffmi_rm *rm, const int *prompt, int n_prompt,
+                                            int max_length, int max_new_tokens,
+                                            int add_special_tokens) {
+  if (!rm || (n_prompt > 0 && !prompt) || n_prompt < 0) return 0;
+  std::vector<int> p(prompt, prompt + n_prompt);
+  return rm->rm.register_new_request(p, max_length, max_new_tokens, add_special_tokens != 0);
+}
+
+extern "C" ffmi_status ffmi_rm_serve_incr_decoding(ffmi_rm *rm, ffmi_model *llm) {
+  if (!rm || !llm || llm->mode != FFMI_MODEL_INC) return FFMI_ERR_INVALID;
+  return rm->rm.serve_incr_decoding(llm);
+}
+
+extern "C" ffmi_status ffmi_rm_serve_spec_infer(ffmi_rm *rm, ffmi_model *llm) {
+  if (!rm || !llm || llm->mode != FFMI_MODEL_TREE) return FFMI_ERR_INVALID;
+  return rm->rm.serve_spec_infer(llm);
+}
+
+extern "C" int ffmi_rm_get_output(ffmi_rm *rm, int64_t guid, int *tokens, int cap) {
+  if (!rm) return -1;
+  const ffmi::GenerationResult *gr = rm->rm.get_generation_result(guid);
+  if (!gr) return -1;
+  const int n = (int)gr->output_tokens.size();
+  for (int i = 0; i < n && i < cap && tokens; ++i) tokens[i] = gr->output_tokens[i];
+  return n;
+}
+
+extern "C" ffmi_status ffmi_rm_get_profile(ffmi_rm *rm, int64_t guid, ffmi_profile *p) {
+  if (!rm || !p) return FFMI_ERR_INVALID;
+  const auto *pi = rm->rm.get_profile(guid);
+  const ffmi::GenerationResult *gr = rm->rm.get_generation_result(guid);
+  if (!pi || !gr) return FFMI_ERR_INVALID;
+  p->llm_decoding_steps = pi->llm_decoding_steps;
+  p->ssm_decoding_steps = pi->ssm_decoding_steps;
+  p->start_us = pi->start_time;
+  p->finish_us = pi->finish_time;
+  p->registration_us = pi->registration_time;
+  p->first_token_us = pi->first_token_time;
+  p->input_len = (int)gr->input_tokens.size();
+  p->output_len = (int)gr->output_tokens.size();
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s) {
+  if (!rm || !s) return FFMI_ERR_INVALID;
+  s->llm_steps = rm->rm.stats.llm_steps;
+  s->ssm_steps = rm->rm.stats.ssm_steps;
+  s->tokens_committed = rm->rm.stats.tokens_committed;
+  s->tree_tokens_verified = rm->rm.stats.tree_tokens_verified;
+  s->wall_us = rm->rm.stats.wall_us;
+  return FFMI_OK;
+}

@@ -1,0 +1,124 @@
+// hash_model.cpp -- scheduler test double (no GPU, TEST USE ONLY).
+//
+// Emulates exactly what the attention kernels see: token ids are stored into
+// per-request cache rows at the packed store slots, TREE commits copy from
+// the previous batch's staging, and each query's "context" is the sequence of
+// cached ids at its visible slots (packed prefix / tree-bitmask rule), in
+// slot order.  The next token is a hash of that context, so:
+//   * incremental decoding yields next = f(prompt + generated so far);
+//   * SpecInfer must reproduce the same tokens (the reference's own
+//     invariant, tests/inference/cpp_inference_tests.sh:183-189) -- any error
+//     in batching, tree build, bitmask, verification or commit lists changes a
+//     context and therefore a token.
+// The SSM flavour ranks f(ctx) first with probability (100-disagree)%.
+#include <array>
+#include <vector>
+
+#include "model.h"
+
+namespace ffmi {
+
+static inline uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+struct HashModel : public ffmi_model {
+  int vocab, max_requests, slots;
+  uint64_t salt;
+  int disagree;
+  std::vector<int> cache;  // [max_requests][slots]
+  std::vector<int> stage;  // previous batch token ids (TREE commits)
+
+  int slot_of(int r, int s) const { return r * slots + s; }
+
+  // returns context hash for each token; -1 entries poison the hash
+  void contexts(const PackedStep &ps, std::vector<uint64_t> *hs) {
+    for (const auto &c : ps.commits) {
+      int v = (c.src_token >= 0 && c.src_token < (int)stage.size()) ? stage[c.src_token] : -7;
+      if (c.depth >= 0 && c.depth < slots) cache[slot_of(c.req, c.depth)] = v;
+    }
+    stage.assign(ps.tokens.size(), -1);
+    for (size_t t = 0; t < ps.tokens.size(); ++t) {
+      const auto &ti = ps.tokens[t];
+      stage[t] = ti.token_id;
+      if (ti.store_slot >= 0) cache[slot_of(ti.req, ti.store_slot)] = ti.token_id;
+    }
+    hs->resize(ps.tokens.size());
+    for (size_t t = 0; t < ps.tokens.size(); ++t) {
+      const auto &ti = ps.tokens[t];
+      const uint64_t *mask =
+          ps.num_mask_reqs ? &ps.masks[(size_t)ti.req * FFMI_MAX_TREE] : nullptr;
+      const int end = std::max(ti.prefix_len, ti.tree_base + ti.tree_len);
+      uint64_t h = 0x243F6A8885A308D3ull;
+      for (int s = 0; s < end; ++s) {
+        bool vis = s < ti.prefix_len;
+        if (!vis && s >= ti.tree_base && s < ti.tree_base + ti.tree_len && mask)
+          vis = (mask[s - ti.tree_base] >> ti.tree_bit) & 1ull;
+        if (!vis) continue;
+        h = mix64(h + (uint64_t)(int64_t)cache[slot_of(ti.req, s)] + 1);
+      }
+      (*hs)[t] = h;
+    }
+  }
+
+  int next_token(uint64_t h) const { return (int)((h >> 17) % (uint64_t)vocab); }
+
+  ffmi_status run_inc(const BatchConfig &bc, InferenceResult *ir) override {
+    PackedStep ps;
+    pack_inc(bc, max_requests, slots, &ps);
+    std::vector<uint64_t> hs;
+    contexts(ps, &hs);
+    for (size_t t = 0; t < hs.size(); ++t) ir->token_ids[t] = next_token(hs[t]);
+    return FFMI_OK;
+  }
+  ffmi_status run_tree(const TreeVerifyBatchConfig &bc, InferenceResult *ir) override {
+    PackedStep ps;
+    pack_tree(bc, max_requests, slots, &ps);
+    std::vector<uint64_t> hs;
+    contexts(ps, &hs);
+    for (size_t t = 0; t < hs.size(); ++t) ir->token_ids[t] = next_token(hs[t]);
+    return FFMI_OK;
+  }
+  ffmi_status run_beam(const BeamSearchBatchConfig &bc, BeamInferenceResult *ir) override {
+    PackedStep ps;
+    pack_beam(bc, max_requests, slots, &ps);
+    std::vector<uint64_t> hs;
+    contexts(ps, &hs);
+    const int k = ps.topk;
+    for (size_t t = 0; t < hs.size(); ++t) {
+      const uint64_t h = hs[t];
+      const int c0 = next_token(h);
+      const int c1 = (int)((c0 + 1 + (h >> 40) % 7) % (uint64_t)vocab);
+      const int c2 = (int)((c1 + 1 + (h >> 45) % 7) % (uint64_t)vocab);
+      const bool agree = (int)(mix64(h ^ salt) % 100) >= disagree;
+      std::array<int, 3> rank = agree ? std::array<int, 3>{c0, c1, c2}
+                                      : std::array<int, 3>{c1, c0, c2};
+      for (int j = 0; j < k; ++j) {
+        ir->token_ids[t * k + j] = rank[j % 3];
+        ir->probs[t * k + j] = 1.0f / (float)(1 << j);
+        ir->parent_id[t * k + j] = 0;
+      }
+    }
+    return FFMI_OK;
+  }
+};
+
+ffmi_status create_hash_model(int vocab, int mode, int max_requests, int max_seq,
+                              int max_tree, uint64_t salt, int disagree_pct,
+                              ffmi_model **out) {
+  if (vocab < 16 || max_requests <= 0 || max_seq <= 0) return FFMI_ERR_INVALID;
+  HashModel *m = new HashModel();
+  m->mode = mode;
+  m->vocab = vocab;
+  m->max_requests = max_requests;
+  m->slots = max_seq + max_tree;
+  m->salt = salt;
+  m->disagree = disagree_pct;
+  m->cache.assign((size_t)max_requests * m->slots, -1);
+  *out = m;
+  return FFMI_OK;
+}
+
+}  // namespace ffmi

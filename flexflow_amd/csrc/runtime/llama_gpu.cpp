@@ -1,0 +1,413 @@
+// llama_gpu.cpp -- LLaMA on MI355X through the C-ABI kernels.
+//
+// Graph per layer (inference/models/llama.cc:55-252):
+//   [rms_norm | residual_rms_norm] -> qkv_proj -> {Inc,Spec,Tree}IncMHA
+//   -> o_proj -> AllReduce -> residual_rms_norm -> gate|up (+SiLU-mul fused)
+//   -> down_proj -> AllReduce
+// tail: residual_rms_norm "norm" -> lm_head -> softmax+argmax (LLM) or
+// softmax+arg_top_k (SSM, llama.cc:277-295).
+// Tensor parallelism (model.cc:3392-3613, linear.cc:1691-1730): qkv/gate/up
+// column-parallel (heads / FFN columns of shard `tp_rank`), o/down
+// row-parallel followed by an RCCL sum all-reduce; norms replicated; lm_head
+// replicated (the reference vocab-shards it and Combines).
+#include <stdio.h>
+#include <string.h>
+
+#include <algorithm>
+#include <cmath>
+
+#include <string>
+#include <vector>
+
+#include "model.h"
+
+namespace ffmi {
+
+namespace {
+
+struct Layer {
+  uint16_t *in_norm = nullptr, *post_norm = nullptr;
+  uint16_t *wqkv = nullptr, *wo = nullptr, *wgu = nullptr, *wd = nullptr;
+  ffmi_attn *attn = nullptr;
+};
+
+struct LlamaGPU : public ffmi_model {
+  ffmi_llama_config c{};
+  ffmi_model_opts o{};
+  int Hl = 0, Fl = 0, d = 0, heads_l = 0, slots = 0;
+  hipStream_t stream = nullptr;
+  std::vector<Layer> layers;
+  uint16_t *embed = nullptr, *final_norm = nullptr, *lm = nullptr;
+  // activations
+  uint16_t *res = nullptr, *h = nullptr, *qkv = nullptr, *att = nullptr, *proj = nullptr,
+           *mlp = nullptr, *logits = nullptr;
+  int32_t *ids_d = nullptr;
+  float *probs_d = nullptr;
+  int32_t *ids_h = nullptr;
+  float *probs_h = nullptr;
+  ffmi_batch_dev *batch = nullptr;
+  PackedStep ps;
+  std::vector<void *> allocs;
+
+  // ---- per-op profiling (HIP events on `stream`) ----
+  enum Cat { GEMM_QKV, GEMM_O, GEMM_GATE_UP, GEMM_DOWN, GEMM_LM_HEAD, ATTENTION, NORM,
+             ALLREDUCE, SAMPLING, EMBED, NCAT };
+  struct ProfRec {
+    int cat;
+    hipEvent_t a, b;
+    double bytes, flops;
+  };
+  struct OpStat {
+    long launches = 0;
+    double ms = 0, bytes = 0, flops = 0;
+  };
+  int prof_level = 0;
+  std::vector<hipEvent_t> ev_pool;
+  size_t ev_used = 0;
+  std::vector<ProfRec> recs;
+  OpStat opstat[NCAT];
+
+  hipEvent_t next_event() {
+    if (ev_used == ev_pool.size()) {
+      hipEvent_t e;
+      (void)hipEventCreate(&e);
+      ev_pool.push_back(e);
+    }
+    return ev_pool[ev_used++];
+  }
+  bool prof_on(int layer, int T) const {
+    if (prof_level == 2) return true;
+    if (prof_level == 1) return T <= 256 && (layer == 0 || layer == c.num_layers / 2);
+    return false;
+  }
+  int prof_begin(bool on) {
+    if (!on) return -1;
+    ProfRec r;
+    r.a = next_event();
+    r.b = next_event();
+    (void)hipEventRecord(r.a, stream);
+    recs.push_back(r);
+    return (int)recs.size() - 1;
+  }
+  void prof_end(int idx, int cat, double bytes, double flops) {
+    if (idx < 0) return;
+    ProfRec &r = recs[idx];
+    r.cat = cat;
+    r.bytes = bytes;
+    r.flops = flops;
+    (void)hipEventRecord(r.b, stream);
+  }
+  void prof_collect() {
+    for (auto &r : recs) {
+      float ms = 0;
+      if (hipEventElapsedTime(&ms, r.a, r.b) != hipSuccess) continue;
+      OpStat &o = opstat[r.cat];
+      o.launches++;
+      o.ms += ms;
+      o.bytes += r.bytes;
+      o.flops += r.flops;
+    }
+    recs.clear();
+    ev_used = 0;
+  }
+  ffmi_status set_profiling(int level) override {
+    prof_level = level;
+    for (auto &o : opstat) o = OpStat();
+    return FFMI_OK;
+  }
+  int op_stats(ffmi_op_stat *out, int cap) override {
+    static const char *names[NCAT] = {"gemm_qkv", "gemm_o_proj", "gemm_gate_up_silu",
+                                      "gemm_down", "gemm_lm_head", "attention", "rmsnorm",
+                                      "allreduce", "softmax_argmax", "embedding"};
+    int n = 0;
+    for (int i = 0; i < NCAT; ++i) {
+      if (opstat[i].launches == 0) continue;
+      if (out && n < cap) {
+        snprintf(out[n].name, sizeof(out[n].name), "%s", names[i]);
+        out[n].launches = opstat[i].launches;
+        out[n].total_ms = opstat[i].ms;
+        out[n].bytes = opstat[i].bytes;
+        out[n].flops = opstat[i].flops;
+      }
+      ++n;
+    }
+    return n;
+  }
+  static double gemm_bytes(int T, int N_w, int N_out, int K) {
+    return 2.0 * ((double)N_w * K + (double)T * K + (double)T * N_out);
+  }
+  double attn_bytes() const {
+    // K and V of every visible slot of each request read once + qkv in + out
+    std::vector<int> kv(o.max_requests, 0);
+    for (const auto &w : ps.work) kv[w.req] = std::max(kv[w.req], w.kv_len);
+    double b = 0;
+    for (int r : kv) b += (double)r * Hl * 2 * 2;
+    return b + (double)ps.tokens.size() * (3 * Hl + Hl) * 2;
+  }
+
+  ~LlamaGPU() override {
+    if (stream) (void)hipStreamSynchronize(stream);
+    for (auto &L : layers) ffmi_attn_destroy(L.attn);
+    for (auto e : ev_pool) (void)hipEventDestroy(e);
+    for (void *p : allocs) (void)hipFree(p);
+    if (ids_h) (void)hipHostFree(ids_h);
+    if (probs_h) (void)hipHostFree(probs_h);
+    ffmi_batch_destroy(batch);
+    if (stream) (void)hipStreamDestroy(stream);
+  }
+
+  template <typename T>
+  ffmi_status alloc(T **p, size_t elems) {
+    if (hipMalloc((void **)p, elems * sizeof(T)) != hipSuccess) {
+      ffmi_set_last_error("model alloc", __FILE__, __LINE__);
+      return FFMI_ERR_OOM;
+    }
+    allocs.push_back(*p);
+    return FFMI_OK;
+  }
+
+  ffmi_status init() {
+    const int H = c.hidden, F = c.intermediate, V = c.vocab_size, P = o.tp_size;
+    FFMI_CHECK(c.num_kv_heads == c.num_heads, FFMI_ERR_UNSUPPORTED);  // MHA
+    FFMI_CHECK(H % c.num_heads == 0 && c.num_heads % P == 0 && F % P == 0, FFMI_ERR_INVALID);
+    d = H / c.num_heads;
+    FFMI_CHECK(d == 64 || d == 128, FFMI_ERR_UNSUPPORTED);
+    heads_l = c.num_heads / P;
+    Hl = heads_l * d;
+    Fl = F / P;
+    FFMI_CHECK(H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0, FFMI_ERR_UNSUPPORTED);
+    FFMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+    const int Tm = o.max_tokens;
+    ffmi_status st;
+#define TRY(x) \
+  do { if ((st = (x)) != FFMI_OK) return st; } while (0)
+    TRY(ffmi_batch_create(Tm, o.max_requests, &batch));
+    TRY(alloc(&res, (size_t)Tm * H));
+    TRY(alloc(&h, (size_t)Tm * H));
+    TRY(alloc(&qkv, (size_t)Tm * 3 * Hl));
+    TRY(alloc(&att, (size_t)Tm * Hl));
+    TRY(alloc(&proj, (size_t)Tm * H));
+    TRY(alloc(&mlp, (size_t)Tm * Fl));
+    TRY(alloc(&logits, (size_t)Tm * V));
+    TRY(alloc(&ids_d, (size_t)Tm * 4));
+    TRY(alloc(&probs_d, (size_t)Tm * 4));
+    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * sizeof(int32_t), 0));
+    FFMI_HIP(hipHostMalloc((void **)&probs_h, (size_t)Tm * 4 * sizeof(float), 0));
+    // weights (seeded synthetic, orc_gen_weight spec), packed for MFMA
+    uint16_t *tmp = nullptr;
+    size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
+    TRY(alloc(&tmp, tmp_elems));
+    auto fill = [&](uint16_t *dst, size_t n, const std::string &name, int kind) {
+      return ffmi_fill_weight(dst, n, name.c_str(), o.weight_seed, kind, (ffmi_stream)stream);
+    };
+    TRY(alloc(&embed, (size_t)V * H));
+    TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0));
+    TRY(alloc(&final_norm, H));
+    TRY(fill(final_norm, H, "model.norm.weight", 1));
+    TRY(alloc(&lm, ffmi_linear_packed_bytes(V, H) / 2));
+    TRY(fill(tmp, (size_t)V * H, "lm_head.weight", 0));
+    FFMI_HIP(launch_pack_weight(tmp, H, 0, 0, V, H, lm, 0, 0, stream));
+    slots = 0;
+    layers.resize(c.num_layers);
+    const int s = o.tp_rank;
+    for (int l = 0; l < c.num_layers; ++l) {
+      Layer &L = layers[l];
+      const std::string p = "model.layers." + std::to_string(l) + ".";
+      TRY(alloc(&L.in_norm, H));
+      TRY(fill(L.in_norm, H, p + "input_layernorm.weight", 1));
+      TRY(alloc(&L.post_norm, H));
+      TRY(fill(L.post_norm, H, p + "post_attention_layernorm.weight", 1));
+      // qkv: [Q_s | K_s | V_s] rows of this shard (file_loader.cc:286-303)
+      const size_t qkv_tiles_bytes = ffmi_linear_packed_bytes(Hl, H);
+      TRY(alloc(&L.wqkv, 3 * qkv_tiles_bytes / 2));
+      const char *names[3] = {"self_attn.q_proj.weight", "self_attn.k_proj.weight",
+                              "self_attn.v_proj.weight"};
+      for (int q = 0; q < 3; ++q) {
+        TRY(fill(tmp, (size_t)H * H, p + names[q], 0));
+        FFMI_HIP(launch_pack_weight(tmp, H, s * Hl, 0, Hl, H, L.wqkv + q * qkv_tiles_bytes / 2, 0,
+                                    0, stream));
+      }
+      // o_proj: row-parallel -> columns [s*Hl, (s+1)*Hl)
+      TRY(alloc(&L.wo, ffmi_linear_packed_bytes(H, Hl) / 2));
+      TRY(fill(tmp, (size_t)H * H, p + "self_attn.o_proj.weight", 0));
+      FFMI_HIP(launch_pack_weight(tmp, H, 0, s * Hl, H, Hl, L.wo, 0, 0, stream));
+      // gate | up: column-parallel, interleaved 16-column tiles
+      TRY(alloc(&L.wgu, 2 * ffmi_linear_packed_bytes(Fl, H) / 2));
+      TRY(fill(tmp, (size_t)F * H, p + "mlp.gate_proj.weight", 0));
+      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 1, 0, stream));
+      TRY(fill(tmp, (size_t)F * H, p + "mlp.up_proj.weight", 0));
+      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 1, 1, stream));
+      // down: row-parallel -> columns [s*Fl, (s+1)*Fl) of [H][F]
+      TRY(alloc(&L.wd, ffmi_linear_packed_bytes(H, Fl) / 2));
+      TRY(fill(tmp, (size_t)H * F, p + "mlp.down_proj.weight", 0));
+      FFMI_HIP(launch_pack_weight(tmp, F, 0, s * Fl, H, Fl, L.wd, 0, 0, stream));
+      ffmi_attn_cfg ac;
+      ac.mode = mode == FFMI_MODEL_TREE ? FFMI_ATTN_TREE
+                                        : (mode == FFMI_MODEL_BEAM ? FFMI_ATTN_SPEC : FFMI_ATTN_INC);
+      ac.num_heads = heads_l;
+      ac.head_dim = d;
+      ac.max_requests = o.max_requests;
+      ac.max_seq_len = o.max_seq_len;
+      ac.max_tree_tokens = mode == FFMI_MODEL_INC ? 0 : o.max_tree_tokens;
+      ac.max_tokens = Tm;
+      ac.qk_scale = 1.0f / sqrtf((float)d);
+      ac.rope_theta = c.rope_theta;
+      TRY(ffmi_attn_create(&ac, &L.attn));
+      int sl = 0;
+      ffmi_attn_kv_ptrs(L.attn, nullptr, nullptr, &sl);
+      slots = sl;
+    }
+    FFMI_HIP(hipStreamSynchronize(stream));
+    // the staging buffer is not needed after init
+    for (auto it = allocs.begin(); it != allocs.end(); ++it)
+      if (*it == tmp) {
+        (void)hipFree(tmp);
+        allocs.erase(it);
+        break;
+      }
+#undef TRY
+    return FFMI_OK;
+  }
+
+  ffmi_status allreduce(uint16_t *buf, size_t n) {
+    if (o.tp_size <= 1) return FFMI_OK;
+    return ffmi_allreduce(o.comm, buf, buf, n, FFMI_F16, (ffmi_stream)stream);
+  }
+
+  // one step of the graph over the uploaded batch; k = results per token
+  ffmi_status forward(int k) {
+    const int T = (int)ps.tokens.size();
+    const int H = c.hidden, V = c.vocab_size;
+    const float eps = c.rms_eps;
+    const ffmi_stream s = (ffmi_stream)stream;
+    ffmi_batch_desc desc;
+    ps.desc(&desc);
+    ffmi_status st;
+#define TRY(x) \
+  do { if ((st = (x)) != FFMI_OK) return st; } while (0)
+    TRY(ffmi_batch_upload(batch, &desc, s));
+    if (T == 0) return FFMI_OK;
+    const bool ptail = prof_on(0, T);
+    int pr = prof_begin(ptail);
+    TRY(ffmi_embedding(batch, embed, res, H, s));
+    prof_end(pr, EMBED, (double)T * H * 4, 0);
+    for (int l = 0; l < c.num_layers; ++l) {
+      Layer &L = layers[l];
+      const bool on = prof_on(l, T);
+      pr = prof_begin(on);
+      if (l == 0)
+        TRY(ffmi_rmsnorm(res, L.in_norm, h, T, H, eps, s));
+      else
+        TRY(ffmi_residual_rmsnorm(res, proj, L.in_norm, res, h, T, H, eps, s));
+      prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 2 : 4), 0);
+      pr = prof_begin(on);
+      TRY(ffmi_linear(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE, s));
+      prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
+      pr = prof_begin(on);
+      if (mode == FFMI_MODEL_TREE)
+        TRY(ffmi_attn_tree(L.attn, batch, qkv, att, s));
+      else if (mode == FFMI_MODEL_BEAM)
+        TRY(ffmi_attn_spec(L.attn, batch, qkv, att, s));
+      else
+        TRY(ffmi_attn_inc(L.attn, batch, qkv, att, s));
+      prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
+      pr = prof_begin(on);
+      TRY(ffmi_linear(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE, s));
+      prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+      pr = prof_begin(on && o.tp_size > 1);
+      TRY(allreduce(proj, (size_t)T * H));
+      prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
+      pr = prof_begin(on);
+      TRY(ffmi_residual_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, s));
+      prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+      pr = prof_begin(on);
+      TRY(ffmi_linear(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL, s));
+      prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
+      pr = prof_begin(on);
+      TRY(ffmi_linear(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE, s));
+      prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+      pr = prof_begin(on && o.tp_size > 1);
+      TRY(allreduce(proj, (size_t)T * H));
+      prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
+    }
+    pr = prof_begin(ptail);
+    TRY(ffmi_residual_rmsnorm(res, proj, final_norm, res, h, T, H, eps, s));
+    prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+    pr = prof_begin(ptail);
+    TRY(ffmi_linear(h, lm, logits, T, V, H, FFMI_EPI_NONE, s));
+    prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
+    pr = prof_begin(ptail);
+    if (k == 1)
+      TRY(ffmi_argmax(logits, T, V, ids_d, probs_d, s));
+    else
+      TRY(ffmi_arg_topk(logits, T, V, k, ids_d, probs_d, s));
+    prof_end(pr, SAMPLING, (double)T * V * 2, 0);
+    FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * sizeof(int32_t), hipMemcpyDeviceToHost,
+                            stream));
+    FFMI_HIP(hipMemcpyAsync(probs_h, probs_d, (size_t)T * k * sizeof(float),
+                            hipMemcpyDeviceToHost, stream));
+    FFMI_HIP(hipStreamSynchronize(stream));
+    if (!recs.empty()) prof_collect();
+#undef TRY
+    return FFMI_OK;
+  }
+
+  ffmi_status run_inc(const BatchConfig &bc, InferenceResult *ir) override {
+    if (mode != FFMI_MODEL_INC) return FFMI_ERR_INVALID;
+    FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
+    pack_inc(bc, o.max_requests, slots, &ps);
+    ffmi_status st = forward(1);
+    if (st != FFMI_OK) return st;
+    memcpy(ir->token_ids, ids_h, bc.num_tokens * sizeof(int32_t));
+    return FFMI_OK;
+  }
+  ffmi_status run_tree(const TreeVerifyBatchConfig &bc, InferenceResult *ir) override {
+    if (mode != FFMI_MODEL_TREE) return FFMI_ERR_INVALID;
+    FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
+    pack_tree(bc, o.max_requests, slots, &ps);
+    ffmi_status st = forward(1);
+    if (st != FFMI_OK) return st;
+    memcpy(ir->token_ids, ids_h, bc.num_tokens * sizeof(int32_t));
+    return FFMI_OK;
+  }
+  ffmi_status run_beam(const BeamSearchBatchConfig &bc, BeamInferenceResult *ir) override {
+    if (mode != FFMI_MODEL_BEAM) return FFMI_ERR_INVALID;
+    FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
+    pack_beam(bc, o.max_requests, slots, &ps);
+    const int k = ps.topk;
+    ffmi_status st = forward(k);
+    if (st != FFMI_OK) return st;
+    const size_t n = (size_t)bc.num_tokens * k;
+    memcpy(ir->token_ids, ids_h, n * sizeof(int32_t));
+    memcpy(ir->probs, probs_h, n * sizeof(float));
+    for (size_t i = 0; i < n; ++i) ir->parent_id[i] = 0;
+    return FFMI_OK;
+  }
+};
+
+}  // namespace
+
+ffmi_status create_llama_gpu(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
+                             ffmi_model **out) {
+  FFMI_CHECK(cfg && o && out, FFMI_ERR_INVALID);
+  FFMI_CHECK(o->tp_size >= 1 && o->tp_rank >= 0 && o->tp_rank < o->tp_size, FFMI_ERR_INVALID);
+  FFMI_CHECK(o->tp_size == 1 || o->comm, FFMI_ERR_INVALID);
+  FFMI_CHECK(o->max_tokens > 0 && o->max_tokens <= BatchConfig::MAX_NUM_TOKENS, FFMI_ERR_INVALID);
+  FFMI_CHECK(o->max_requests > 0 && o->max_requests <= BatchConfig::MAX_NUM_REQUESTS,
+             FFMI_ERR_INVALID);
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return FFMI_ERR_NO_DEVICE;
+  LlamaGPU *m = new LlamaGPU();
+  m->mode = o->mode;
+  m->c = *cfg;
+  m->o = *o;
+  ffmi_status st = m->init();
+  if (st != FFMI_OK) {
+    delete m;
+    return st;
+  }
+  *out = m;
+  return FFMI_OK;
+}
+
+}  // namespace ffmi

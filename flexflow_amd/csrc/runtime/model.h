@@ -1,0 +1,68 @@
+// model.h -- model handles behind the RequestManager (C handle ffmi_model).
+//
+// The reference builds a Legion operator graph per InferenceMode
+// (inference/models/llama.cc:23-317) and runs it with
+// InferenceManager::inference (inference_manager.cc:408-468).  Here a model
+// is a C++ object that owns its weights and per-layer attention handles and
+// runs one step of a BatchConfig through the C-ABI kernels in graph order.
+#pragma once
+#include <vector>
+
+#include "../ffmi_internal.h"
+#include "batch_config.h"
+
+namespace ffmi {
+
+// Per-step device metadata derived from a BatchConfig (what the kernels read).
+struct PackedStep {
+  std::vector<ffmi_token_info> tokens;
+  std::vector<ffmi_attn_work> work;
+  std::vector<ffmi_commit_info> commits;
+  std::vector<uint64_t> masks;  // [num_mask_reqs][FFMI_MAX_TREE]
+  int num_mask_reqs = 0;
+  int topk = 1;  // BEAM: results per token (beam width)
+  void desc(ffmi_batch_desc *d) const;
+};
+
+// KV-slot / visibility packing, one per reference attention op:
+//  INC  : store_kv_cache, inc_multihead_self_attention.cu:35-61 (slot = depth),
+//         causal visibility (generation + prompt paths)
+//  TREE : update_tree_branch_kv_cache_fused, tree_inc...cu:433-478 (slot =
+//         first_depth + local), commit list tree_inc...cu:335-396, bitmask
+//         visibility tree_inc...cu:150-170 / prompt causal :166-168
+//  BEAM : spec_inc_store_kv_cache, spec_inc...cu:311-358 (slot = prompt_size
+//         + non_tree + tree_size - 1 - this_layer_size + local), bitmask
+//         visibility with query_token = prompt_size+tree_size-1-branches+qi
+//         (spec_inc...cu:145-170), causal prompt path :461-679
+void pack_inc(const BatchConfig &bc, int max_requests, int slots, PackedStep *out);
+void pack_tree(const TreeVerifyBatchConfig &bc, int max_requests, int slots, PackedStep *out);
+void pack_beam(const BeamSearchBatchConfig &bc, int max_requests, int slots, PackedStep *out);
+
+}  // namespace ffmi
+
+struct ffmi_model {
+  int mode = FFMI_MODEL_INC;
+  virtual ~ffmi_model() {}
+  virtual ffmi_status run_inc(const ffmi::BatchConfig &bc, ffmi::InferenceResult *ir) = 0;
+  virtual ffmi_status run_tree(const ffmi::TreeVerifyBatchConfig &bc,
+                               ffmi::InferenceResult *ir) = 0;
+  virtual ffmi_status run_beam(const ffmi::BeamSearchBatchConfig &bc,
+                               ffmi::BeamInferenceResult *ir) = 0;
+  virtual ffmi_status set_profiling(int level) {
+    (void)level;
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  virtual int op_stats(ffmi_op_stat *out, int cap) {
+    (void)out;
+    (void)cap;
+    return 0;
+  }
+};
+
+namespace ffmi {
+ffmi_status create_llama_gpu(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
+                             ffmi_model **out);
+ffmi_status create_hash_model(int vocab, int mode, int max_requests, int max_seq,
+                              int max_tree, uint64_t salt, int disagree_pct,
+                              ffmi_model **out);
+}  // namespace ffmi

@@ -1,0 +1,917 @@
+// request_manager.cpp -- continuous batching and the SpecInfer token-tree
+// scheduler, restated from src/runtime/request_manager.cc (reference
+// @2025-01-17).  Each function cites the reference lines whose behaviour it
+// reproduces.  Deliberate differences (documented in DESIGN.md):
+//  * bit operations on BitMask words are 64-bit (1ull << j); the reference's
+//    `1 << j` on int breaks for trees deeper than 31 tokens (quirk 6);
+//  * no tokenizer: requests carry token ids (the parity unit);
+//  * no PEFT / finetuning requests;
+//  * more than one SSM is rejected, as the reference asserts
+//    (merge_dfs_trees, request_manager.cc:2823-2827).
+#include "request_manager.h"
+
+#include <assert.h>
+#include <stdio.h>
+
+#include <algorithm>
+#include <chrono>
+
+namespace ffmi {
+
+double now_us() {
+  using namespace std::chrono;
+  return (double)duration_cast<nanoseconds>(steady_clock::now().time_since_epoch()).count() *
+         1e-3;
+}
+
+static BatchLimits g_limits;
+BatchLimits &batch_limits() { return g_limits; }
+int BatchConfig::max_requests_per_batch() { return g_limits.max_requests_per_batch; }
+int BatchConfig::max_tokens_per_batch() { return g_limits.max_tokens_per_batch; }
+int BatchConfig::max_spec_tree_token_num() { return g_limits.max_spec_tree_token_num; }
+int BatchConfig::max_sequence_length() { return g_limits.max_sequence_length; }
+int BatchConfig::max_verify_tokens_per_batch() {
+  return g_limits.max_tokens_per_batch +
+         g_limits.max_spec_tree_token_num * g_limits.max_requests_per_batch;
+}
+
+BatchConfig::BatchConfig() {
+  for (int i = 0; i < MAX_NUM_REQUESTS; ++i) {
+    request_completed[i] = true;
+    request_running[i] = false;
+  }
+}
+
+int BatchConfig::num_active_requests() const {
+  int n = 0;
+  for (int i = 0; i < max_requests_per_batch(); ++i) n += !request_completed[i];
+  return n;
+}
+
+RequestManager::RequestManager() {}
+
+void RequestManager::apply_limits() const {
+  g_limits.max_requests_per_batch = max_requests_per_batch;
+  g_limits.max_tokens_per_batch = max_tokens_per_batch;
+  g_limits.max_spec_tree_token_num = max_spec_tree_token_num;
+  g_limits.max_sequence_length = max_sequence_length;
+}
+
+// request_manager.cc:168-171
+bool RequestManager::push_spec_infer_tree_width(int w) {
+  if (w > BeamSearchBatchConfig::MAX_BEAM_WIDTH || w < 1) return false;
+  // nodes per tree layer = product of the widths so far; the reference
+  // asserts it stays <= MAX_SPECULATIVE_TREE_BRANCHES at run time
+  // (request_manager.cc:1685-1687) -- reject such a sequence up front
+  int nodes = w;
+  for (int x : spec_infer_tree_width) nodes *= x;
+  if (nodes > BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES) return false;
+  spec_infer_tree_width.push_back(w);
+  return true;
+}
+
+// request_manager.cc:334-441 (tokenizer replaced by token ids)
+RequestManager::RequestGuid RequestManager::register_new_request(
+    const std::vector<int> &prompt, int max_length, int max_new_tokens,
+    bool add_special_tokens) {
+  Request request;
+  request.status = Request::PENDING;
+  request.guid = next_available_guid++;
+  request.max_length = max_length;
+  request.max_new_tokens = max_new_tokens;
+  request.add_special_tokens = add_special_tokens;
+  if (request.max_length == -1 && request.max_new_tokens == -1)
+    request.max_length = max_sequence_length - 1;
+  if (request.max_length != -1 && request.max_new_tokens != -1) request.max_length = -1;
+  if (bos_token_id >= 0 && request.add_special_tokens) request.tokens.push_back(bos_token_id);
+  if (request.max_new_tokens != -1)
+    request.max_length = (int)prompt.size() + request.max_new_tokens;
+  if ((int)prompt.size() >= max_sequence_length) return 0;
+  if (request.max_length >= max_sequence_length) return 0;
+  request.tokens.insert(request.tokens.end(), prompt.begin(), prompt.end());
+  request.initial_len = (int)request.tokens.size();
+  if (!ssm_models.empty()) request.beam_trees.resize(ssm_models.size());
+  pending_infr_request_queue.push_back(request);
+  all_requests[request.guid] = request;
+  GenerationResult gr;
+  gr.guid = request.guid;
+  gr.input_tokens = request.tokens;
+  gr.output_tokens = request.tokens;
+  request_generation_results[request.guid] = gr;
+  ProfileInfo pi;
+  pi.registration_time = now_us();
+  profiling_requests[request.guid] = pi;
+  return request.guid;
+}
+
+bool RequestManager::is_eos_token(int token_id) const {
+  for (int e : eos_token_ids)
+    if (e == token_id) return true;
+  return false;
+}
+
+// request_manager.cc:645-657
+bool RequestManager::check_inf_req_completion(const BatchConfig &old_bc, int i) {
+  Request &request = all_requests[old_bc.requestsInfo[i].request_guid];
+  if ((int)request.tokens.size() >= old_bc.requestsInfo[i].max_length) return true;
+  return is_eos_token(request.tokens.back());
+}
+
+void RequestManager::complete_request(Request &request) {
+  request.status = Request::COMPLETED;
+  GenerationResult &gr = request_generation_results[request.guid];
+  gr.output_tokens = request.tokens;
+  ProfileInfo &pi = profiling_requests[request.guid];
+  pi.finish_time = now_us();
+  num_processed_requests++;
+  if (verbose)
+    printf("[ffmi] guid(%lld) done: len %zu llm_steps %d latency %.1f us\n",
+           (long long)request.guid, request.tokens.size(), pi.llm_decoding_steps,
+           pi.finish_time - pi.start_time);
+}
+
+// request_manager.cc:713-1135 (inference requests only)
+BatchConfig RequestManager::prepare_next_batch(const BatchConfig &old_bc,
+                                               const InferenceResult &result) {
+  // Step 1: append the result of the previous step
+  for (int i = 0; i < old_bc.num_tokens; i++) {
+    const RequestGuid guid = old_bc.requestsInfo[old_bc.tokensInfo[i].request_index].request_guid;
+    Request &request = all_requests[guid];
+    if (old_bc.tokensInfo[i].abs_depth_in_request + 1 < (int)request.tokens.size()) continue;
+    assert(old_bc.tokensInfo[i].abs_depth_in_request + 1 == (int)request.tokens.size());
+    ProfileInfo &pi = profiling_requests[guid];
+    if (!pi.first_token_time_set) {
+      pi.first_token_time = now_us();
+      pi.first_token_time_set = true;
+    }
+    request.tokens.push_back(result.token_ids[i]);
+  }
+  // Step 2: carry on running requests
+  BatchConfig new_bc;
+  int num_generation_tokens = 0;
+  int num_active_req = -1;
+  const int batch_size = max_requests_per_batch;
+  for (int i = 0; i < batch_size; i++) {
+    if (old_bc.request_completed[i]) continue;
+    Request &request = all_requests[old_bc.requestsInfo[i].request_guid];
+    const int processed = old_bc.requestsInfo[i].first_token_depth_in_request +
+                          old_bc.requestsInfo[i].num_tokens_in_batch;
+    assert(processed < (int)request.tokens.size());
+    if (check_inf_req_completion(old_bc, i)) {
+      if (is_eos_token(request.tokens.back())) request.tokens.pop_back();
+      complete_request(request);
+      continue;
+    }
+    auto &R = new_bc.requestsInfo[i];
+    new_bc.request_completed[i] = false;
+    R.first_token_depth_in_request = processed;
+    R.first_token_offset_in_batch = new_bc.num_tokens;
+    R.request_guid = old_bc.requestsInfo[i].request_guid;
+    R.max_length = old_bc.requestsInfo[i].max_length;
+    num_active_req++;
+    new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+    if (R.first_token_depth_in_request + 1 == (int)request.tokens.size()) {
+      R.num_tokens_in_batch = 1;  // decoding
+      num_generation_tokens++;
+      R.prompt_phase = false;
+    } else {
+      // prompt chunk; keep room for the decoding requests behind it (:866-890)
+      int space_for_incr_dec_requests = 0;
+      for (int ii = i + 1; ii < batch_size; ii++) {
+        if (old_bc.request_completed[ii]) continue;
+        if (!check_inf_req_completion(old_bc, ii)) space_for_incr_dec_requests++;
+      }
+      R.num_tokens_in_batch = std::min(
+          max_tokens_per_batch - new_bc.num_tokens - space_for_incr_dec_requests,
+          (int)request.tokens.size() - R.first_token_depth_in_request);
+      R.prompt_phase = true;
+    }
+    for (int j = 0; j < R.num_tokens_in_batch; j++) {
+      const int depth = R.first_token_depth_in_request + j;
+      new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+      new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = depth;
+      new_bc.tokensInfo[new_bc.num_tokens].token_id = request.tokens[depth];
+      new_bc.num_tokens++;
+    }
+    profiling_requests[R.request_guid].llm_decoding_steps++;
+  }
+  new_bc.num_generation_tokens = num_generation_tokens;
+  // Step 3: admit new requests into free slots (:910-963)
+  for (int i = 0; i < batch_size; i++) {
+    if (!new_bc.request_completed[i]) continue;
+    if (pending_infr_request_queue.empty() || new_bc.num_tokens >= max_tokens_per_batch) continue;
+    Request new_request = pending_infr_request_queue.front();
+    pending_infr_request_queue.pop_front();
+    auto &R = new_bc.requestsInfo[i];
+    R.first_token_depth_in_request = 0;
+    R.first_token_offset_in_batch = new_bc.num_tokens;
+    R.request_guid = new_request.guid;
+    R.num_tokens_in_batch = std::min(max_tokens_per_batch - new_bc.num_tokens,
+                                     (int)new_request.tokens.size());
+    R.max_length = new_request.max_length;
+    R.prompt_phase = true;
+    new_bc.request_completed[i] = false;
+    num_active_req++;
+    new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+    ProfileInfo &pi = profiling_requests[new_request.guid];
+    pi.llm_decoding_steps = 1;
+    pi.start_time = now_us();
+    for (int j = 0; j < R.num_tokens_in_batch; j++) {
+      new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+      new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = j;
+      new_bc.tokensInfo[new_bc.num_tokens].token_id = new_request.tokens[j];
+      new_bc.num_tokens++;
+    }
+    if (new_bc.num_tokens == max_tokens_per_batch) break;
+  }
+  return new_bc;
+}
+
+// ---------------------------------------------------------------------------
+// SpecInfer: request init phase (request_manager.cc:1170-1579)
+// ---------------------------------------------------------------------------
+BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
+    const TreeVerifyBatchConfig &old_bc, const InferenceResult &result, int model_id) {
+  BeamSearchBatchConfig new_bc;
+  new_bc.num_tokens = 0;
+  new_bc.model_id = model_id;
+  int result_index = 0;
+  int num_active_req = -1;
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (old_bc.request_completed[i]) continue;
+    const RequestGuid guid = old_bc.requestsInfo[i].request_guid;
+    Request &request = all_requests[guid];
+    std::vector<TokenDepth> tree_outputs;
+    committed_tokens[guid].clear();
+    const int root_abs_depth = (int)request.tokens.size() - 1;
+    while (result_index < old_bc.num_tokens &&
+           old_bc.tokensInfo[result_index].request_index == i) {
+      const int abs_depth = old_bc.tokensInfo[result_index].abs_depth_in_request;
+      const int token_id = result.token_ids[result_index];
+      if (request.status == Request::PENDING) {
+        committed_tokens[guid].emplace_back(abs_depth, result_index);
+      } else if (abs_depth >= root_abs_depth) {
+        tree_outputs.emplace_back(token_id, abs_depth + 1);
+        committed_tokens[guid].emplace_back(abs_depth, result_index);
+      }
+      result_index++;
+    }
+    if (request.status == Request::RUNNING) {
+      std::vector<TokenDepth> verified_tokens =
+          traverse_verify_tree(guid, dfs_tree_inputs.at(guid), tree_outputs);
+      stats.tokens_committed += (long)verified_tokens.size();
+      if ((int)(verified_tokens.size() + request.tokens.size()) >= request.max_length) {
+        for (const auto &tp : verified_tokens)
+          if (tp.second < request.max_length) request.tokens.push_back(tp.first);
+        complete_request(request);
+        new_bc.request_completed[i] = true;
+        new_bc.request_running[i] = false;
+        dfs_tree_inputs.erase(guid);
+      } else {
+        new_bc.request_completed[i] = false;
+        new_bc.request_running[i] = true;
+        num_active_req++;
+        auto &R = new_bc.requestsInfo[i];
+        R.first_token_depth_in_request = verified_tokens.front().second;
+        R.first_token_offset_in_batch = new_bc.num_tokens;
+        R.request_guid = guid;
+        R.max_length = old_bc.requestsInfo[i].max_length;
+        R.num_tokens_in_batch = (int)verified_tokens.size();
+        new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+        const int new_max_depth =
+            R.max_length - R.first_token_depth_in_request - (int)verified_tokens.size();
+        auto &B = new_bc.beamRequestsInfo[i];
+        B.current_depth = 1;
+        profiling_requests[guid].ssm_decoding_steps = 0;
+        R.prompt_phase = true;
+        B.beam_size = spec_infer_tree_width.size() > 0 ? spec_infer_tree_width[0] : 1;
+        B.max_depth = std::min(new_max_depth, BeamSearchBatchConfig::MAX_BEAM_DEPTH);
+        for (int j = 0; j < BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES; j++) {
+          B.parent_id[j] = 0;
+          B.probs[j] = 1;
+        }
+        B.sub_request_num = 1;
+        new_bc.sub_requests[i] = 1;
+        updateBitMask(new_bc.causalMask[i], (int)verified_tokens.size(),
+                      (int)request.tokens.size());
+        for (size_t j = 0; j < verified_tokens.size(); j++) {
+          const auto &tk = verified_tokens[j];
+          new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+          new_bc.tokensInfo[new_bc.num_tokens].token_id = tk.first;
+          new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = tk.second;
+          new_bc.beamTokenInfo[new_bc.num_tokens].sub_request_index = 0;
+          new_bc.num_tokens++;
+          request.tokens.push_back(tk.first);
+          if (new_bc.num_tokens == max_tokens_per_batch) break;
+        }
+      }
+    } else if (request.status == Request::PENDING) {
+      new_bc.request_completed[i] = false;
+      new_bc.request_running[i] = false;
+      num_active_req++;
+      assert(request.ssm_cache_size == request.initial_len);
+      auto &R = new_bc.requestsInfo[i];
+      R.first_token_depth_in_request = request.ssm_cache_size;
+      R.first_token_offset_in_batch = new_bc.num_tokens;
+      R.request_guid = guid;
+      R.max_length = old_bc.requestsInfo[i].max_length;
+      R.num_tokens_in_batch = 0;
+      new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+      auto &B = new_bc.beamRequestsInfo[i];
+      B.current_depth = 1;
+      const int steps = profiling_requests[guid].ssm_decoding_steps;
+      B.beam_size = (int)spec_infer_tree_width.size() > steps ? spec_infer_tree_width[steps] : 1;
+      B.max_depth = 0;
+      for (int j = 0; j < BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES; j++) {
+        B.parent_id[j] = 0;
+        B.probs[j] = 1;
+      }
+      B.sub_request_num = 1;
+      new_bc.sub_requests[i] = 1;
+    } else {
+      assert(false && "request status is not RUNNING or PENDING");
+    }
+  }
+  // admit new requests (:1497-1571)
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (!new_bc.request_completed[i]) continue;
+    if (pending_infr_request_queue.empty() || new_bc.num_tokens >= max_tokens_per_batch) continue;
+    Request new_request = pending_infr_request_queue.front();
+    pending_infr_request_queue.pop_front();
+    num_active_req++;
+    auto &R = new_bc.requestsInfo[i];
+    R.first_token_depth_in_request = 0;
+    R.first_token_offset_in_batch = new_bc.num_tokens;
+    R.request_guid = new_request.guid;
+    R.num_tokens_in_batch =
+        std::min(max_tokens_per_batch - new_bc.num_tokens, (int)new_request.tokens.size());
+    R.max_length = new_request.max_length;
+    new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+    ProfileInfo &pi = profiling_requests[new_request.guid];
+    pi.llm_decoding_steps = 0;
+    pi.ssm_decoding_steps = 0;
+    pi.start_time = now_us();
+    auto &B = new_bc.beamRequestsInfo[i];
+    B.beam_size = spec_infer_tree_width.size() > 0 ? spec_infer_tree_width[0] : 1;
+    B.current_depth = 1;
+    B.max_depth = std::min(BeamSearchBatchConfig::MAX_BEAM_DEPTH,
+                           max_tokens_per_batch - R.num_tokens_in_batch - 1);
+    for (int j = 0; j < BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES; j++) {
+      B.parent_id[j] = 0;
+      B.probs[j] = 1;
+    }
+    new_bc.request_completed[i] = false;
+    R.prompt_phase = true;
+    B.sub_request_num = 1;
+    new_bc.sub_requests[i] = 1;
+    for (int j = 0; j < R.num_tokens_in_batch; j++) {
+      new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+      new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = j;
+      new_bc.tokensInfo[new_bc.num_tokens].token_id = new_request.tokens[j];
+      new_bc.beamTokenInfo[new_bc.num_tokens].sub_request_index = 0;
+      new_bc.num_tokens++;
+    }
+    initBitMask(new_bc.causalMask[i], R.num_tokens_in_batch);
+    all_requests[new_request.guid].status = Request::PENDING;
+    all_requests[new_request.guid].ssm_cache_size = R.num_tokens_in_batch;
+    new_bc.request_running[i] = false;
+    if (new_bc.num_tokens == max_tokens_per_batch) break;
+  }
+  new_bc.num_generation_tokens = 0;
+  return new_bc;
+}
+
+// ---------------------------------------------------------------------------
+// SpecInfer: beam (SSM) phase (request_manager.cc:1610-1892)
+// ---------------------------------------------------------------------------
+BeamSearchBatchConfig RequestManager::prepare_next_batch_beam(
+    const BeamSearchBatchConfig &old_bc, const BeamInferenceResult &result) {
+  store_beam_metadata(old_bc, result);
+  BeamSearchBatchConfig new_bc;
+  new_bc.model_id = old_bc.model_id;
+  int num_generation_tokens = 0;
+  int num_active_req = -1;
+  // running requests first
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (old_bc.request_completed[i] || !old_bc.request_running[i]) continue;
+    num_active_req++;
+    Request &request = all_requests[old_bc.requestsInfo[i].request_guid];
+    const int processed = old_bc.requestsInfo[i].first_token_depth_in_request +
+                          old_bc.requestsInfo[i].num_tokens_in_batch;
+    auto &R = new_bc.requestsInfo[i];
+    auto &B = new_bc.beamRequestsInfo[i];
+    const auto &OB = old_bc.beamRequestsInfo[i];
+    new_bc.request_completed[i] = false;
+    R.first_token_depth_in_request = processed;
+    R.first_token_offset_in_batch = new_bc.num_tokens;
+    R.request_guid = old_bc.requestsInfo[i].request_guid;
+    R.max_length = old_bc.requestsInfo[i].max_length;
+    const int steps = ++profiling_requests[request.guid].ssm_decoding_steps;
+    new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+    B.beam_size = (int)spec_infer_tree_width.size() > steps ? spec_infer_tree_width[steps] : 1;
+    B.max_depth = OB.max_depth;
+    new_bc.sub_requests[i] = old_bc.sub_requests[i] * B.beam_size;
+    B.sub_request_num = OB.sub_request_num * OB.beam_size;
+    assert(B.sub_request_num <= BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES);
+    assert(request.status == Request::RUNNING);
+    B.current_depth = OB.current_depth + 1;
+    new_bc.request_running[i] = true;
+    update_beam_metadata(new_bc, old_bc, request.beam_trees.at(old_bc.model_id), i);
+    if (R.first_token_depth_in_request >= (int)request.tokens.size())
+      R.num_tokens_in_batch = 1;
+    new_bc.causalMask[i] = old_bc.causalMask[i];
+    appendBitMask(new_bc.causalMask[i], B.sub_request_num, OB.beam_size, OB.sub_request_num,
+                  request.beam_trees[old_bc.model_id], OB.current_depth);
+    for (int j = 0; j < R.num_tokens_in_batch; j++) {
+      const int depth = R.first_token_depth_in_request + j;
+      for (int k = 0; k < B.sub_request_num; k++) {
+        new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+        new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = depth;
+        new_bc.tokensInfo[new_bc.num_tokens].token_id = B.tokens[k];
+        new_bc.beamTokenInfo[new_bc.num_tokens].sub_request_index = k;
+        new_bc.num_tokens++;
+        num_generation_tokens++;
+      }
+    }
+  }
+  new_bc.speculative_request_num = num_active_req + 1;
+  // pending (prompt-loading) requests
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (old_bc.request_completed[i] || old_bc.request_running[i]) continue;
+    num_active_req++;
+    Request &request = all_requests[old_bc.requestsInfo[i].request_guid];
+    const int processed = old_bc.requestsInfo[i].first_token_depth_in_request +
+                          old_bc.requestsInfo[i].num_tokens_in_batch;
+    auto &R = new_bc.requestsInfo[i];
+    auto &B = new_bc.beamRequestsInfo[i];
+    const auto &OB = old_bc.beamRequestsInfo[i];
+    new_bc.request_completed[i] = false;
+    R.first_token_depth_in_request = processed;
+    R.first_token_offset_in_batch = new_bc.num_tokens;
+    R.request_guid = old_bc.requestsInfo[i].request_guid;
+    R.max_length = old_bc.requestsInfo[i].max_length;
+    new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+    B.beam_size = 1;
+    B.max_depth = OB.max_depth;
+    new_bc.sub_requests[i] = 1;
+    B.sub_request_num = OB.sub_request_num;
+    assert(request.status == Request::PENDING);
+    B.current_depth = OB.current_depth;
+    new_bc.request_running[i] = false;
+    new_bc.causalMask[i] = old_bc.causalMask[i];
+    R.prompt_phase = true;
+    if (R.first_token_depth_in_request >= (int)request.tokens.size()) {
+      R.num_tokens_in_batch = 0;
+      new_bc.causalMask[i].this_layer_size = 0;
+      B.sub_request_num = 0;
+      B.beam_size = 1;
+    } else {
+      R.num_tokens_in_batch =
+          std::min(max_tokens_per_batch - new_bc.num_tokens - max_requests_per_batch + i,
+                   (int)request.tokens.size() - R.first_token_depth_in_request);
+      request.ssm_cache_size += R.num_tokens_in_batch;
+      appendPendingRequest(new_bc.causalMask[i], R.num_tokens_in_batch);
+    }
+    for (int j = 0; j < R.num_tokens_in_batch; j++) {
+      const int depth = R.first_token_depth_in_request + j;
+      for (int k = 0; k < B.sub_request_num; k++) {
+        new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+        new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = depth;
+        new_bc.tokensInfo[new_bc.num_tokens].token_id =
+            request.tokens[request.tokens.size() - R.num_tokens_in_batch + j];
+        new_bc.beamTokenInfo[new_bc.num_tokens].sub_request_index = k;
+        new_bc.num_tokens++;
+      }
+    }
+  }
+  new_bc.num_generation_tokens = num_generation_tokens;
+  return new_bc;
+}
+
+// ---------------------------------------------------------------------------
+// SpecInfer: verify (LLM) phase (request_manager.cc:1923-2215)
+// ---------------------------------------------------------------------------
+TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
+    const std::vector<BeamSearchBatchConfig> &old_batches) {
+  assert(!old_batches.empty());
+  TreeVerifyBatchConfig new_bc;
+  new_bc.num_tokens_to_commit = 0;
+  new_bc.num_tokens = 0;
+  const int max_verify = get_max_verify_tokens_per_batch();
+  int max_prompt_load_size = max_verify;
+  const BeamSearchBatchConfig &b0 = old_batches.at(0);
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (b0.request_completed[i]) continue;
+    if (b0.request_running[i])
+      max_prompt_load_size -= (BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1);
+    else
+      max_prompt_load_size -= 1;
+  }
+  int num_active_req = -1;
+  for (int i = 0; i < max_requests_per_batch; i++) {
+    if (b0.request_completed[i]) continue;
+    num_active_req++;
+    const RequestGuid guid = b0.requestsInfo[i].request_guid;
+    Request &request = all_requests[guid];
+    profiling_requests[guid].llm_decoding_steps += 1;
+    auto &R = new_bc.requestsInfo[i];
+    if (request.status == Request::RUNNING) {
+      new_bc.request_running[i] = true;
+      std::vector<std::vector<TokenDepth>> all_dfs_trees;
+      for (size_t j = 0; j < old_batches.size(); j++)
+        all_dfs_trees.push_back(
+            traverse_beam_tree(old_batches.at(j), i, (int)request.tokens.size() - 1));
+      std::vector<TokenDepth> tree =
+          merge_dfs_trees(all_dfs_trees, (int)request.tokens.size() - 1, guid);
+      R.first_token_depth_in_request = tree.front().second;
+      R.first_token_offset_in_batch = new_bc.num_tokens;
+      R.request_guid = guid;
+      R.max_length = b0.requestsInfo[i].max_length;
+      new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+      new_bc.causalMask[i] = b0.causalMask[i];
+      R.num_tokens_in_batch = 0;
+      new_bc.request_completed[i] = false;
+      auto it = committed_tokens.find(guid);
+      if (it != committed_tokens.end()) {
+        for (const auto &ct : it->second) {
+          auto &c = new_bc.committed_tokens[new_bc.num_tokens_to_commit];
+          c.token_index = ct.second;
+          c.request_index = i;
+          c.token_depth = ct.first;
+          new_bc.num_tokens_to_commit++;
+          request.llm_cache_size++;
+        }
+      }
+      // the root: the last verified token
+      new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+      new_bc.tokensInfo[new_bc.num_tokens].token_id = request.tokens.back();
+      new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request =
+          (int)request.tokens.size() - 1;
+      new_bc.num_tokens++;
+      R.num_tokens_in_batch++;
+      assert(new_bc.num_tokens <= max_verify);
+      R.first_token_depth_in_request = (int)request.tokens.size() - 1;
+      bool cutLayer = false;
+      for (size_t j = 1; j < tree.size(); j++) {
+        new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+        new_bc.tokensInfo[new_bc.num_tokens].token_id = tree[j].first;
+        new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = tree[j].second;
+        new_bc.num_tokens++;
+        R.num_tokens_in_batch++;
+        if (new_bc.num_tokens == max_verify && j != tree.size() - 1) {
+          cutLayer = true;
+          break;
+        }
+      }
+      if (cutLayer) {  // drop the partially included last layer
+        const int total_tokens = new_bc.num_tokens;
+        for (int j = total_tokens - 1; j >= 1; j--) {
+          new_bc.num_tokens--;
+          R.num_tokens_in_batch--;
+          if (new_bc.tokensInfo[j].abs_depth_in_request !=
+              new_bc.tokensInfo[j - 1].abs_depth_in_request)
+            break;
+        }
+      }
+      stats.tree_tokens_verified += R.num_tokens_in_batch;
+    } else if (request.status == Request::PENDING) {
+      new_bc.request_running[i] = false;
+      auto it = committed_tokens.find(guid);
+      if (it != committed_tokens.end()) {
+        for (const auto &ct : it->second) {
+          auto &c = new_bc.committed_tokens[new_bc.num_tokens_to_commit];
+          c.token_index = ct.second;
+          c.request_index = i;
+          c.token_depth = ct.first;
+          new_bc.num_tokens_to_commit++;
+          request.llm_cache_size++;
+        }
+      }
+      new_bc.causalMask[i] = b0.causalMask[i];
+      R.first_token_depth_in_request = request.llm_cache_size;
+      R.first_token_offset_in_batch = new_bc.num_tokens;
+      R.request_guid = guid;
+      R.max_length = b0.requestsInfo[i].max_length;
+      new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
+      new_bc.request_completed[i] = false;
+      R.num_tokens_in_batch = std::min(max_prompt_load_size,
+                                       request.initial_len - R.first_token_depth_in_request);
+      max_prompt_load_size -= R.num_tokens_in_batch;
+      if (request.llm_cache_size < request.initial_len) {
+        for (int j = 0; j < R.num_tokens_in_batch; j++) {
+          new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+          new_bc.tokensInfo[new_bc.num_tokens].token_id = request.tokens[request.llm_cache_size + j];
+          new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = request.llm_cache_size + j;
+          new_bc.num_tokens++;
+        }
+        assert(new_bc.num_tokens <= max_verify);
+        if (R.num_tokens_in_batch + request.llm_cache_size >= request.initial_len) {
+          request.status = Request::RUNNING;
+          new_bc.request_running[i] = true;
+          R.prompt_phase = true;
+          dfs_tree_inputs[guid] = std::vector<TokenDepth>{
+              TokenDepth(request.tokens.back(), (int)request.tokens.size() - 1)};
+        }
+      } else if (max_verify - new_bc.num_tokens > 0) {
+        // whole prompt cached: launch the request with its last token
+        request.status = Request::RUNNING;
+        new_bc.request_running[i] = true;
+        new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
+        new_bc.tokensInfo[new_bc.num_tokens].token_id = request.tokens.back();
+        new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request =
+            (int)request.tokens.size() - 1;
+        new_bc.num_tokens++;
+        R.num_tokens_in_batch++;
+        R.prompt_phase = true;
+        dfs_tree_inputs[guid] = std::vector<TokenDepth>{
+            TokenDepth(request.tokens.back(), (int)request.tokens.size() - 1)};
+      }
+    } else {
+      assert(false && "request status is not RUNNING or PENDING");
+    }
+  }
+  return new_bc;
+}
+
+// request_manager.cc:2217-2325
+void RequestManager::store_beam_metadata(const BeamSearchBatchConfig &old_bc,
+                                         const BeamInferenceResult &result) {
+  if (old_bc.num_tokens <= 0) return;
+  RequestGuid guid = old_bc.requestsInfo[old_bc.tokensInfo[0].request_index].request_guid;
+  int start_depth = old_bc.tokensInfo[0].abs_depth_in_request;
+  int result_index = 0;
+  for (int i = 0; i <= old_bc.num_tokens; i++) {
+    if (i == old_bc.num_tokens ||
+        old_bc.requestsInfo[old_bc.tokensInfo[i].request_index].request_guid != guid) {
+      const int index = old_bc.tokensInfo[i - 1].request_index;
+      const int beam_size = old_bc.beamRequestsInfo[index].beam_size;
+      const int leaf_node_num = old_bc.beamRequestsInfo[index].sub_request_num * beam_size;
+      const int depth = old_bc.beamRequestsInfo[index].current_depth;
+      result_index += (old_bc.tokensInfo[i - 1].abs_depth_in_request - start_depth) * beam_size;
+      Request &request = all_requests[old_bc.requestsInfo[index].request_guid];
+      if (old_bc.requestsInfo[index].num_tokens_in_batch == 0) continue;
+      auto &tree = request.beam_trees.at(old_bc.model_id);
+      if (depth == 1) {
+        tree.treeLayers[0].tokens[0] = request.tokens.back();
+        tree.treeLayers[0].probs[0] = 1;
+        tree.treeLayers[0].parent_ids[0] = -1;
+        tree.treeLayers[0].nodes_num_this_layer = 1;
+      }
+      tree.treeLayers[depth].nodes_num_this_layer = leaf_node_num;
+      for (int beam_id = 0; beam_id < leaf_node_num; beam_id++) {
+        tree.treeLayers[depth].tokens[beam_id] = result.token_ids[result_index];
+        tree.treeLayers[depth].probs[beam_id] = result.probs[result_index];
+        tree.treeLayers[depth].parent_ids[beam_id] = result.parent_id[result_index];
+        result_index += 1;
+      }
+      if (i < old_bc.num_tokens) {
+        guid = old_bc.requestsInfo[old_bc.tokensInfo[i].request_index].request_guid;
+        start_depth = old_bc.tokensInfo[i].abs_depth_in_request;
+      }
+    }
+  }
+}
+
+// request_manager.cc:2327-2380
+void RequestManager::update_beam_metadata(BeamSearchBatchConfig &new_bc,
+                                          const BeamSearchBatchConfig &old_bc,
+                                          Request::BeamTree &tree, int request_index) {
+  (void)old_bc;
+  const int depth = new_bc.beamRequestsInfo[request_index].current_depth - 1;
+  const int leaf_node_num = new_bc.beamRequestsInfo[request_index].sub_request_num;
+  if (new_bc.beamRequestsInfo[request_index].current_depth == 1) return;
+  for (int j = 0; j < leaf_node_num; j++) {
+    new_bc.beamRequestsInfo[request_index].parent_id[j] = tree.treeLayers[depth].parent_ids[j];
+    new_bc.beamRequestsInfo[request_index].probs[j] = tree.treeLayers[depth].probs[j];
+    new_bc.beamRequestsInfo[request_index].tokens[j] = tree.treeLayers[depth].tokens[j];
+  }
+}
+
+// request_manager.cc:2382-2390
+void RequestManager::initBitMask(BatchConfig::BitMask &bitmask, int initLength) {
+  assert(initLength > 0);
+  bitmask.non_tree_cache_size = 0;
+  bitmask.tree_size = 1;
+  bitmask.prompt_size = initLength;
+  bitmask.this_layer_size = initLength;
+}
+
+// request_manager.cc:2393-2412
+void RequestManager::updateBitMask(BatchConfig::BitMask &bitmask, int initLength,
+                                   int non_tree_size) {
+  assert(initLength <= BatchConfig::MAX_SPEC_TREE_TOKEN_NUM);
+  assert(initLength >= 1);
+  bitmask.non_tree_cache_size = non_tree_size + initLength - 1;
+  bitmask.tree_size = 1;
+  bitmask.this_layer_size = initLength;
+  bitmask.prompt_size = 1;
+  for (int i = 0; i < bitmask.prompt_size; i++)
+    for (int j = i; j < bitmask.prompt_size; j++) bitmask.mask[i] |= (1ull << j);
+}
+
+// request_manager.cc:2415-2423
+void RequestManager::appendPendingRequest(BatchConfig::BitMask &bitmask, int initLength) {
+  assert(initLength > 0);
+  bitmask.non_tree_cache_size = 0;
+  bitmask.tree_size = 1;
+  bitmask.prompt_size += initLength;
+  bitmask.this_layer_size = initLength;
+}
+
+// request_manager.cc:2426-2476
+void RequestManager::appendBitMask(BatchConfig::BitMask &bitmask, int newNodes,
+                                   int preBeamSize, int old_sub_num,
+                                   const Request::BeamTree &tree, int currentDepth) {
+  (void)preBeamSize;
+  (void)old_sub_num;
+  const int pre_tree_size = bitmask.tree_size;
+  bitmask.tree_size += newNodes;
+  bitmask.this_layer_size = newNodes;
+  assert(bitmask.tree_size <= BatchConfig::MAX_SPEC_TREE_TOKEN_NUM);
+  for (int i = 0; i < bitmask.prompt_size; i++)
+    for (int j = pre_tree_size; j < bitmask.tree_size; j++) bitmask.mask[i] |= (1ull << j);
+  int token_idx = bitmask.prompt_size;
+  int new_nodes_start_idx = pre_tree_size;
+  for (int i = 1; i < currentDepth; i++) {
+    new_nodes_start_idx = pre_tree_size;
+    const int nodes_this_layer = tree.treeLayers[i].nodes_num_this_layer;
+    for (int j = 0; j < nodes_this_layer; j++) {
+      const int group_size = newNodes / nodes_this_layer;
+      for (int k = 0; k < group_size; k++) {
+        bitmask.mask[token_idx] |= (1ull << new_nodes_start_idx);
+        new_nodes_start_idx += 1;
+      }
+      token_idx += 1;
+    }
+  }
+  assert(token_idx == pre_tree_size);
+  assert(currentDepth <= 1 || new_nodes_start_idx == bitmask.tree_size);
+  for (int i = token_idx; i < bitmask.tree_size; i++) bitmask.mask[i] |= (1ull << i);
+}
+
+// request_manager.cc:2583-2741: greedy path acceptance over the layer-order
+// serialized tree; returns the verified (token, depth) list and rewrites the
+// request's commit list to the accepted nodes.
+std::vector<RequestManager::TokenDepth> RequestManager::traverse_verify_tree(
+    size_t guid, const std::vector<TokenDepth> &input, const std::vector<TokenDepth> &output) {
+  std::vector<TokenDepth> verifiedTree;
+  std::vector<std::pair<int, int>> new_committed_tokens;
+  assert(input.size() >= output.size());
+  std::vector<int> treeLayers(input.size());
+  int node_num = 1, layer_num = 0;
+  for (size_t t = 0; t < input.size(); t++) {
+    if (t == input.size() - 1 || input.at(t + 1).second != input.at(t).second) {
+      treeLayers[layer_num++] = node_num;
+      node_num = 1;
+    } else {
+      node_num++;
+    }
+  }
+  bool findFirst = false;
+  layer_num = -1;
+  int first_layer_slot = 0;
+  int processed_whole_layer_tokens = 0;
+  const auto &ct = committed_tokens.at((RequestGuid)guid);
+  for (size_t i = 0; i < output.size(); i++) {
+    const auto &in = input.at(i);
+    const auto &out = output.at(i);
+    if (i == 0 || input.at(i - 1).second != input.at(i).second) {
+      layer_num += 1;
+      processed_whole_layer_tokens += i == 0 ? 0 : treeLayers[layer_num - 1];
+    }
+    if (i == 0) {
+      verifiedTree.push_back(out);
+      new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
+      assert(ct.at(i).first == in.second);
+      continue;
+    }
+    if (in.first == verifiedTree.back().first && in.second == verifiedTree.back().second) {
+      if (findFirst) {
+        const int layer_slot = (int)i - processed_whole_layer_tokens;
+        if (first_layer_slot == layer_slot) {
+          verifiedTree.push_back(out);
+          new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
+        }
+      } else {
+        verifiedTree.push_back(out);
+        first_layer_slot = (int)i - processed_whole_layer_tokens;
+        findFirst = true;
+        new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
+      }
+      assert(ct.at(i).first == in.second);
+    }
+  }
+  committed_tokens[(RequestGuid)guid] = new_committed_tokens;
+  return verifiedTree;
+}
+
+// request_manager.cc:2743-2815: layer-order serialization of the beam tree
+std::vector<RequestManager::TokenDepth> RequestManager::traverse_beam_tree(
+    const BeamSearchBatchConfig &old_bc, int request_index, int first_token_depth) {
+  const RequestGuid guid = old_bc.requestsInfo[request_index].request_guid;
+  Request &request = all_requests[guid];
+  const auto &tree = request.beam_trees.at(old_bc.model_id);
+  std::vector<TokenDepth> serializedTree;
+  for (int i = 0; i <= old_bc.beamRequestsInfo[request_index].max_depth; i++)
+    for (int j = 0; j < tree.treeLayers[i].nodes_num_this_layer; j++)
+      serializedTree.push_back(std::make_pair(tree.treeLayers[i].tokens[j], i));
+  for (auto &p : serializedTree) p.second += first_token_depth;
+  return serializedTree;
+}
+
+// request_manager.cc:2817-2878 (one SSM: the tree is used as is)
+std::vector<RequestManager::TokenDepth> RequestManager::merge_dfs_trees(
+    const std::vector<std::vector<TokenDepth>> &trees, int root_depth, RequestGuid guid) {
+  (void)root_depth;
+  assert(trees.size() == 1 && "currently using one ssm");
+  dfs_tree_inputs[guid] = trees.at(0);
+  return trees.at(0);
+}
+
+bool RequestManager::all_done() const {
+  if (!pending_infr_request_queue.empty()) return false;
+  for (const auto &kv : all_requests)
+    if (kv.second.status != Request::COMPLETED) return false;
+  return true;
+}
+
+const GenerationResult *RequestManager::get_generation_result(RequestGuid guid) const {
+  auto it = request_generation_results.find(guid);
+  return it == request_generation_results.end() ? nullptr : &it->second;
+}
+
+const RequestManager::ProfileInfo *RequestManager::get_profile(RequestGuid guid) const {
+  auto it = profiling_requests.find(guid);
+  return it == profiling_requests.end() ? nullptr : &it->second;
+}
+
+// request_manager.cc:3012-3080 (synchronous: one batch in flight)
+ffmi_status RequestManager::serve_incr_decoding(ffmi_model *llm) {
+  if (!llm) return FFMI_ERR_INVALID;
+  apply_limits();
+  stats = Stats();
+  const double t0 = now_us();
+  BatchConfig *bc = new BatchConfig();
+  InferenceResult *ir = new InferenceResult();
+  ffmi_status st = FFMI_OK;
+  while (!all_done()) {
+    BatchConfig *next = new BatchConfig(prepare_next_batch(*bc, *ir));
+    delete bc;
+    bc = next;
+    if (bc->num_tokens == 0) {
+      if (all_done()) break;
+      st = FFMI_ERR_INVALID;  // nothing schedulable but requests remain
+      break;
+    }
+    st = llm->run_inc(*bc, ir);
+    if (st != FFMI_OK) break;
+    stats.llm_steps++;
+  }
+  delete bc;
+  delete ir;
+  stats.wall_us = now_us() - t0;
+  return st;
+}
+
+// request_manager.cc:3083-3173
+ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
+  if (!llm) return FFMI_ERR_INVALID;
+  if (ssm_models.size() != 1) return FFMI_ERR_UNSUPPORTED;
+  apply_limits();
+  stats = Stats();
+  const double t0 = now_us();
+  TreeVerifyBatchConfig *tree_bc = new TreeVerifyBatchConfig();
+  InferenceResult *tree_ir = new InferenceResult();
+  BeamInferenceResult *beam_ir = new BeamInferenceResult();
+  std::vector<BeamSearchBatchConfig> *beam_vec = new std::vector<BeamSearchBatchConfig>();
+  ffmi_status st = FFMI_OK;
+  while (!all_done()) {
+    beam_vec->assign(ssm_models.size(), prepare_next_batch_init(*tree_bc, *tree_ir, 0));
+    if (all_done()) break;
+    for (size_t s = 0; s < ssm_models.size() && st == FFMI_OK; s++) {
+      for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {
+        st = ssm_models[s]->run_beam((*beam_vec)[s], beam_ir);
+        if (st != FFMI_OK) break;
+        stats.ssm_steps++;
+        (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+      }
+    }
+    if (st != FFMI_OK) break;
+    *tree_bc = prepare_next_batch_verify(*beam_vec);
+    if (tree_bc->num_tokens == 0 && !all_done()) {
+      st = FFMI_ERR_INVALID;
+      break;
+    }
+    st = llm->run_tree(*tree_bc, tree_ir);
+    if (st != FFMI_OK) break;
+    stats.llm_steps++;
+  }
+  delete tree_bc;
+  delete tree_ir;
+  delete beam_ir;
+  delete beam_vec;
+  stats.wall_us = now_us() - t0;
+  return st;
+}
+
+}  // namespace ffmi

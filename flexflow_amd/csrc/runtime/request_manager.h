@@ -1,0 +1,158 @@
+// request_manager.h -- continuous batching + SpecInfer token-tree scheduler.
+//
+// API-compatible restatement of include/flexflow/request_manager.h:119-358
+// (RequestManager) without Legion: the prepare_next_batch* functions take
+// and return the BatchConfig structs directly, and the serve loops run in the
+// caller's thread until every registered request has completed (the
+// reference runs the same loop as a background Legion task and generate()
+// blocks on per-request promises, request_manager.cc:2880-2989).
+#pragma once
+#include <deque>
+#include <map>
+#include <string>
+#include <unordered_map>
+#include <utility>
+#include <vector>
+
+#include "batch_config.h"
+#include "model.h"
+
+namespace ffmi {
+
+struct Request {
+  enum Status { PENDING = 101, RUNNING = 102, COMPLETED = 103, FINISHING = 104 };
+  BatchConfig::RequestGuid guid = 0;
+  int max_length = -1;
+  int max_new_tokens = -1;
+  bool add_special_tokens = true;
+  int initial_len = 0;
+  int ssm_cache_size = 0;
+  int llm_cache_size = 0;
+  Status status = PENDING;
+  std::vector<BatchConfig::TokenId> tokens;
+  struct BeamTree {
+    struct Layer {
+      BatchConfig::TokenId tokens[BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES];
+      int parent_ids[BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES];
+      float probs[BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES];
+      int nodes_num_this_layer = 0;
+    };
+    Layer treeLayers[BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1];
+  };
+  std::vector<BeamTree> beam_trees;
+};
+
+struct GenerationResult {
+  BatchConfig::RequestGuid guid = 0;
+  std::vector<BatchConfig::TokenId> input_tokens, output_tokens;
+};
+
+class RequestManager {
+ public:
+  using RequestGuid = BatchConfig::RequestGuid;
+  using TokenId = BatchConfig::TokenId;
+  using TokenDepth = std::pair<TokenId, int>;
+
+  RequestManager();
+  void set_max_requests_per_batch(int n) { max_requests_per_batch = n; }
+  void set_max_tokens_per_batch(int n) { max_tokens_per_batch = n; }
+  void set_max_spec_tree_token_num(int n) { max_spec_tree_token_num = n; }
+  void set_max_sequence_length(int n) { max_sequence_length = n; }
+  int get_max_requests_per_batch() const { return max_requests_per_batch; }
+  int get_max_tokens_per_batch() const { return max_tokens_per_batch; }
+  int get_max_spec_tree_token_num() const { return max_spec_tree_token_num; }
+  int get_max_sequence_length() const { return max_sequence_length; }
+  int get_max_verify_tokens_per_batch() const {
+    return max_tokens_per_batch + max_spec_tree_token_num * max_requests_per_batch;
+  }
+  bool push_spec_infer_tree_width(int w);
+  void register_tokenizer(int bos, const std::vector<int> &eos) {
+    bos_token_id = bos;
+    eos_token_ids = eos;
+  }
+  int register_ssm_model(ffmi_model *m) {
+    ssm_models.push_back(m);
+    return (int)ssm_models.size() - 1;
+  }
+  size_t get_num_ssms() const { return ssm_models.size(); }
+  void set_verbose(bool v) { verbose = v; }
+
+  RequestGuid register_new_request(const std::vector<int> &prompt, int max_length,
+                                   int max_new_tokens, bool add_special_tokens);
+
+  // bitmask helpers (request_manager.cc:2382-2517)
+  void initBitMask(BatchConfig::BitMask &bitmask, int initLength);
+  void appendPendingRequest(BatchConfig::BitMask &bitmask, int initLength);
+  void appendBitMask(BatchConfig::BitMask &bitmask, int newNodes, int preBeamSize,
+                     int old_sub_num, const Request::BeamTree &tree, int currentDepth);
+  void updateBitMask(BatchConfig::BitMask &bitmask, int initLength, int non_tree_size);
+
+  bool is_eos_token(int token_id) const;
+  bool check_inf_req_completion(const BatchConfig &old_bc, int i);
+
+  BatchConfig prepare_next_batch(const BatchConfig &bc, const InferenceResult &result);
+  BeamSearchBatchConfig prepare_next_batch_init(const TreeVerifyBatchConfig &old_bc,
+                                                const InferenceResult &result, int model_id);
+  BeamSearchBatchConfig prepare_next_batch_beam(const BeamSearchBatchConfig &old_bc,
+                                                const BeamInferenceResult &result);
+  TreeVerifyBatchConfig prepare_next_batch_verify(
+      const std::vector<BeamSearchBatchConfig> &old_batches);
+
+  void store_beam_metadata(const BeamSearchBatchConfig &old_bc,
+                           const BeamInferenceResult &result);
+  void update_beam_metadata(BeamSearchBatchConfig &new_bc, const BeamSearchBatchConfig &old_bc,
+                            Request::BeamTree &tree, int request_index);
+  std::vector<TokenDepth> traverse_beam_tree(const BeamSearchBatchConfig &old_bc,
+                                             int request_index, int first_token_depth);
+  std::vector<TokenDepth> merge_dfs_trees(const std::vector<std::vector<TokenDepth>> &trees,
+                                          int root_depth, RequestGuid guid);
+  std::vector<TokenDepth> traverse_verify_tree(size_t guid,
+                                               const std::vector<TokenDepth> &input,
+                                               const std::vector<TokenDepth> &output);
+
+  ffmi_status serve_incr_decoding(ffmi_model *llm);
+  ffmi_status serve_spec_infer(ffmi_model *llm);
+
+  bool all_done() const;
+  const GenerationResult *get_generation_result(RequestGuid guid) const;
+
+  struct ProfileInfo {
+    int llm_decoding_steps = 0;
+    int ssm_decoding_steps = 0;
+    double start_time = 0, finish_time = 0;
+    double registration_time = 0, first_token_time = 0;
+    bool first_token_time_set = false;
+  };
+  const ProfileInfo *get_profile(RequestGuid guid) const;
+  struct Stats {
+    long llm_steps = 0, ssm_steps = 0, tokens_committed = 0, tree_tokens_verified = 0;
+    double wall_us = 0;
+  } stats;
+
+ private:
+  void complete_request(Request &request);
+  void apply_limits() const;
+
+  int max_requests_per_batch = 8;
+  int max_tokens_per_batch = 128;
+  int max_spec_tree_token_num = 23;
+  int max_sequence_length = 512;
+  std::vector<int> spec_infer_tree_width;
+  int bos_token_id = 1;
+  std::vector<int> eos_token_ids;
+  bool verbose = false;
+
+  std::deque<Request> pending_infr_request_queue;
+  std::map<RequestGuid, Request> all_requests;
+  std::map<RequestGuid, GenerationResult> request_generation_results;
+  RequestGuid next_available_guid = 1000000;
+  std::unordered_map<RequestGuid, std::vector<TokenDepth>> dfs_tree_inputs;
+  std::unordered_map<RequestGuid, std::vector<std::pair<int, int>>> committed_tokens;
+  std::vector<ffmi_model *> ssm_models;
+  std::map<RequestGuid, ProfileInfo> profiling_requests;
+  size_t num_processed_requests = 0;
+};
+
+double now_us();
+
+}  // namespace ffmi

@@ -1,0 +1,173 @@
+"""Serving API over libffmi.so, mirroring the reference's RequestManager /
+FFModel::generate surface (include/flexflow/request_manager.h:119-358,
+python/flexflow/serve/serve.py LLM/SSM).  All work happens in the C++
+runtime and HIP kernels; this file only marshals arguments.
+"""
+import ctypes
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+from . import ffmi as F
+
+
+class Model:
+    """A LLaMA model on one GPU (one TP shard).  mode: "inc" (incremental
+    decoding LLM), "tree" (SpecInfer verify LLM) or "beam" (SSM)."""
+
+    MODES = {"inc": F.MODEL_INC, "beam": F.MODEL_BEAM, "tree": F.MODEL_TREE}
+
+    def __init__(self, config: dict, mode: str = "inc", *, max_requests=8, max_tokens=128,
+                 max_seq_len=512, max_tree_tokens=23, weight_seed=20250117, tp_rank=0,
+                 tp_size=1, comm=None):
+        L = F.lib()
+        self.config = dict(config)
+        self.mode = mode
+        cfg = F.LlamaConfig.from_dict(config)
+        opts = F.ModelOpts(self.MODES[mode], tp_rank, tp_size, comm.handle if comm else None,
+                           max_requests, max_tokens, max_seq_len, max_tree_tokens, weight_seed, 0)
+        h = ctypes.c_void_p()
+        F.check(L.ffmi_model_create(ctypes.byref(cfg), ctypes.byref(opts), ctypes.byref(h)),
+                "ffmi_model_create")
+        self.handle = h
+
+    def set_profiling(self, level: int):
+        F.check(F.lib().ffmi_model_set_profiling(self.handle, level), "set_profiling")
+
+    def op_stats(self):
+        n = F.lib().ffmi_model_op_stats(self.handle, None, 0)
+        arr = (F.OpStat * max(n, 1))()
+        F.lib().ffmi_model_op_stats(self.handle, arr, n)
+        return {a.name.decode(): dict(launches=a.launches, ms=a.total_ms, bytes=a.bytes,
+                                      flops=a.flops) for a in arr[:n]}
+
+    def close(self):
+        if getattr(self, "handle", None):
+            F.lib().ffmi_model_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+
+def set_device(dev: int):
+    F.check(F.lib().ffmi_set_device(dev), "set_device")
+
+
+class HashModel(Model):
+    """Scheduler test double (CPU only, see ffmi_test_hash_model_create)."""
+
+    def __init__(self, vocab=1000, mode="inc", *, max_requests=8, max_seq_len=512,
+                 max_tree_tokens=23, salt=0, disagree_pct=0):
+        self.mode = mode
+        h = ctypes.c_void_p()
+        F.check(F.lib().ffmi_test_hash_model_create(vocab, self.MODES[mode], max_requests,
+                                                    max_seq_len, max_tree_tokens, salt,
+                                                    disagree_pct, ctypes.byref(h)),
+                "hash model")
+        self.handle = h
+
+
+class Comm:
+    """RCCL communicator for tensor parallelism (one process per GPU)."""
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        F.check(F.lib().ffmi_comm_unique_id(buf), "unique id")
+        return buf.raw
+
+    def __init__(self, uid: bytes, nranks: int, rank: int):
+        h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(uid, 128)
+        F.check(F.lib().ffmi_comm_create(buf, nranks, rank, ctypes.byref(h)), "comm create")
+        self.handle = h
+
+    def close(self):
+        if getattr(self, "handle", None):
+            F.lib().ffmi_comm_destroy(self.handle)
+            self.handle = None
+
+
+@dataclass
+class GenerationResult:
+    guid: int
+    input_tokens: List[int]
+    output_tokens: List[int]
+    llm_decoding_steps: int = 0
+    ssm_decoding_steps: int = 0
+    latency_us: float = 0.0
+    ttft_us: float = 0.0
+
+
+class RequestManager:
+    def __init__(self, max_requests_per_batch=8, max_tokens_per_batch=128,
+                 max_spec_tree_token_num=23, max_sequence_length=512, bos_token_id=1,
+                 eos_token_ids=(), spec_tree_width=(), verbose=False):
+        self._eos = F.int_array(list(eos_token_ids))
+        self._widths = F.int_array(list(spec_tree_width))
+        cfg = F.RMConfig(max_requests_per_batch, max_tokens_per_batch, max_spec_tree_token_num,
+                         max_sequence_length, bos_token_id, self._eos, len(eos_token_ids),
+                         self._widths, len(spec_tree_width), int(verbose))
+        h = ctypes.c_void_p()
+        F.check(F.lib().ffmi_rm_create(ctypes.byref(cfg), ctypes.byref(h)), "rm create")
+        self.handle = h
+        self.guids: List[int] = []
+        self._ssms = []
+
+    def close(self):
+        if getattr(self, "handle", None):
+            F.lib().ffmi_rm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+    def register_ssm_model(self, ssm: Model):
+        F.check(F.lib().ffmi_rm_register_ssm(self.handle, ssm.handle), "register ssm")
+        self._ssms.append(ssm)
+
+    def register_new_request(self, prompt: List[int], max_length=-1, max_new_tokens=-1,
+                             add_special_tokens=True) -> int:
+        arr = F.int_array(list(prompt))
+        g = F.lib().ffmi_rm_register_request(self.handle, arr, len(prompt), max_length,
+                                             max_new_tokens, int(add_special_tokens))
+        if g > 0:
+            self.guids.append(g)
+        return g
+
+    def serve_incr_decoding(self, llm: Model):
+        F.check(F.lib().ffmi_rm_serve_incr_decoding(self.handle, llm.handle), "serve incr")
+
+    def serve_spec_infer(self, llm: Model):
+        F.check(F.lib().ffmi_rm_serve_spec_infer(self.handle, llm.handle), "serve spec")
+
+    def get_generation_result(self, guid: int) -> GenerationResult:
+        L = F.lib()
+        n = L.ffmi_rm_get_output(self.handle, guid, None, 0)
+        buf = (ctypes.c_int * max(n, 1))()
+        L.ffmi_rm_get_output(self.handle, guid, buf, n)
+        p = F.Profile()
+        F.check(L.ffmi_rm_get_profile(self.handle, guid, ctypes.byref(p)), "profile")
+        out = list(buf[:n])
+        return GenerationResult(guid, out[:p.input_len], out, p.llm_decoding_steps,
+                                p.ssm_decoding_steps, p.finish_us - p.start_us,
+                                p.first_token_us - p.registration_us)
+
+    def stats(self) -> F.ServeStats:
+        s = F.ServeStats()
+        F.check(F.lib().ffmi_rm_get_stats(self.handle, ctypes.byref(s)), "stats")
+        return s
+
+
+def generate(rm: RequestManager, llm: Model, prompts, max_length=-1, max_new_tokens=-1,
+             spec: Optional[bool] = None):
+    """FFModel::generate (request_manager.cc:2880-2911): register, serve, collect."""
+    guids = [rm.register_new_request(p, max_length=max_length, max_new_tokens=max_new_tokens)
+             for p in prompts]
+    if spec is None:
+        spec = llm.mode == "tree"
+    if spec:
+        rm.serve_spec_infer(llm)
+    else:
+        rm.serve_incr_decoding(llm)
+    return [rm.get_generation_result(g) if g > 0 else None for g in guids]

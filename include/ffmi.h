@@ -1,0 +1,304 @@
+/*
+ * ffmi.h -- C ABI of the MI355X-native SpecInfer hot path (libffmi.so).
+ *
+ * Drop-in boundary for the reference's Op/OpMeta kernel-wrapper layer
+ * (hugolatendresse/FlexFlow @ 2025-01-17).  Each entry point names the
+ * reference interface it replaces.  Plain C types only: device pointers,
+ * sizes, an explicit hipStream_t.  Activations are caller-owned; KV caches and
+ * workspaces are handle-owned (the reference's Meta objects own them too,
+ * inc_multihead_self_attention.cu:1621-1807).  No exceptions cross the ABI:
+ * every call returns an ffmi_status (the reference asserts instead,
+ * cuda_helper.h:40-58; a caller shim may assert on != FFMI_OK).
+ *
+ * Threading: a handle is used by one host thread at a time, like an OpMeta
+ * (one GPU task thread per processor in Legion).  All device work is ordered
+ * on the stream argument.
+ */
+#ifndef FFMI_H_
+#define FFMI_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *ffmi_stream; /* == hipStream_t */
+
+typedef enum {
+  FFMI_OK = 0,
+  FFMI_ERR_INVALID = 1,     /* bad argument / shape the kernels do not cover */
+  FFMI_ERR_HIP = 2,         /* HIP runtime error */
+  FFMI_ERR_NCCL = 3,        /* RCCL error */
+  FFMI_ERR_OOM = 4,         /* device allocation failed */
+  FFMI_ERR_UNSUPPORTED = 5, /* head size / mode not built */
+  FFMI_ERR_NO_DEVICE = 6    /* no gfx950 device visible */
+} ffmi_status;
+
+typedef enum { FFMI_F16 = 0, FFMI_F32 = 1, FFMI_I32 = 2 } ffmi_dtype;
+
+/* Attention mode == the reference op that the handle replaces. */
+typedef enum {
+  FFMI_ATTN_INC = 0,  /* IncMultiHeadSelfAttention     (inc_decoding)  */
+  FFMI_ATTN_SPEC = 1, /* SpecIncMultiHeadSelfAttention (SSM beam step) */
+  FFMI_ATTN_TREE = 2  /* TreeIncMultiHeadSelfAttention (LLM verify)    */
+} ffmi_attn_mode;
+
+/* ------------------------------------------------------------------------ */
+/* Device batch metadata                                                     */
+/* ------------------------------------------------------------------------ */
+/* One packed blob per step replaces the reference's per-step H2D copies of
+ * tokensInfo / requestsInfo / causalMask / committed_tokens / beam info
+ * (request_manager.cu:23-159, ~83-150 KB per GPU per step): the host packs
+ * only what the step uses, in the form the kernels read.                    */
+
+typedef struct {
+  int32_t token_id;   /* input token (embedding row)                         */
+  int32_t pos;        /* RoPE position = abs_depth_in_request                */
+  int32_t req;        /* request slot (KV-cache row)                         */
+  int32_t store_slot; /* KV-cache slot this token's K/V goes to (-1: none)   */
+  int32_t prefix_len; /* keys [0, prefix_len) are visible to this token      */
+  int32_t tree_base;  /* first tree slot                                     */
+  int32_t tree_len;   /* tree slots [tree_base, tree_base+tree_len) ...      */
+  int32_t tree_bit;   /* ... visible iff mask[req][slot-tree_base] bit set   */
+} ffmi_token_info;
+
+typedef struct {
+  int32_t req;     /* request slot                                         */
+  int32_t q_start; /* first batch token of this work item                  */
+  int32_t q_count; /* tokens in the item (<= FFMI_ATTN_QTILE)              */
+  int32_t kv_len;  /* keys scanned: [0, kv_len)                            */
+} ffmi_attn_work;
+
+typedef struct {
+  int32_t src_token; /* token index in the PREVIOUS verify batch (staging) */
+  int32_t req;       /* request slot                                       */
+  int32_t depth;     /* destination KV slot (token depth)                  */
+  int32_t pad;
+} ffmi_commit_info;
+
+#define FFMI_ATTN_QTILE 16
+#define FFMI_MAX_TREE 64
+
+/* Host-side description of one step (pointers into host memory). */
+typedef struct {
+  int32_t num_tokens;
+  int32_t num_work;
+  int32_t num_commits;
+  int32_t num_mask_reqs;        /* rows in `masks` (indexed by req slot)    */
+  const ffmi_token_info *tokens;   /* [num_tokens]                          */
+  const ffmi_attn_work *work;      /* [num_work]                            */
+  const ffmi_commit_info *commits; /* [num_commits]                         */
+  const uint64_t *masks;           /* [num_mask_reqs][FFMI_MAX_TREE]        */
+} ffmi_batch_desc;
+
+typedef struct ffmi_batch_dev ffmi_batch_dev; /* device copy + pinned staging */
+
+ffmi_status ffmi_batch_create(int max_tokens, int max_requests, ffmi_batch_dev **out);
+void ffmi_batch_destroy(ffmi_batch_dev *b);
+/* Replaces RM_LOAD_TOKENS / RM_LOAD_BATCH_CONFIG tasks
+ * (request_manager.cu:23-159): one async H2D copy of the used bytes. */
+ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_desc *desc,
+                              ffmi_stream stream);
+
+/* ------------------------------------------------------------------------ */
+/* Attention (replaces src/ops/{inc,spec_inc,tree_inc}_multihead_self_attention) */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int mode;            /* ffmi_attn_mode                                     */
+  int num_heads;       /* heads on this shard                                */
+  int head_dim;        /* 64 or 128                                          */
+  int max_requests;    /* KV rows                                            */
+  int max_seq_len;     /* committed slots per request (S)                    */
+  int max_tree_tokens; /* extra slots for tree / spec (S' = S + tree)        */
+  int max_tokens;      /* batch capacity (staging rows for TREE commits)     */
+  float qk_scale;      /* 1/sqrt(head_dim) (qk_prod_scaling)                 */
+  float rope_theta;    /* HF rotate-half RoPE base                           */
+} ffmi_attn_cfg;
+
+typedef struct ffmi_attn ffmi_attn;
+
+/* init_task -> IncMultiHeadSelfAttentionMeta ctor (inc_mha.cu:1621-1807) */
+ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **out);
+void ffmi_attn_destroy(ffmi_attn *h);
+/* IncMultiHeadSelfAttention::inference_kernel_wrapper (inc_mha.h:115-119) */
+ffmi_status ffmi_attn_inc(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                          void *out, ffmi_stream stream);
+/* SpecIncMultiHeadSelfAttention::inference_kernel_wrapper (spec_inc_mha.h:102) */
+ffmi_status ffmi_attn_spec(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                           void *out, ffmi_stream stream);
+/* TreeIncMultiHeadSelfAttention::inference_kernel_wrapper (tree_inc_mha.h:104);
+ * commits the previous verify batch's accepted K/V first (tree_inc...cu:583-606) */
+ffmi_status ffmi_attn_tree(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
+                           void *out, ffmi_stream stream);
+/* test hooks: raw KV cache pointers and layout ([req][head][slot][d] for K,
+ * [req][head][d][slot] for V, slots = max_seq_len + max_tree_tokens) */
+ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *slots);
+
+/* ------------------------------------------------------------------------ */
+/* Linear (replaces Kernels::Linear::inference_kernel_wrapper,               */
+/* linear_kernels.h:54-62; cublasGemmEx at linear_kernels.cu:510-528)        */
+/* ------------------------------------------------------------------------ */
+typedef enum {
+  FFMI_EPI_NONE = 0,    /* Y = X W^T                                           */
+  FFMI_EPI_SILU_MUL = 1 /* W = [gate;up] (2N rows): Y = silu(X Wg^T) * (X Wu^T)
+                           (fuses SigmoidSiluMulti, sigmoid_silu_multi.cu:37-47) */
+} ffmi_epilogue;
+
+/* Bytes of the MFMA-swizzled weight for an [N][K] fp16 matrix. */
+size_t ffmi_linear_packed_bytes(int out_dim, int in_dim);
+/* [N][K] row-major fp16 (HF layout) -> MFMA fragment order.  For
+ * FFMI_EPI_SILU_MUL pass gate and up separately; they are interleaved. */
+ffmi_status ffmi_linear_pack_weight(const void *W, int out_dim, int in_dim,
+                                    void *W_packed, ffmi_stream stream);
+ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, int out_dim,
+                                     int in_dim, void *W_packed, ffmi_stream stream);
+/* Y[T][out] = X[T][in] . W^T, fp16 in/out, fp32 accumulate. */
+ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
+                        int out_dim, int in_dim, int epilogue, ffmi_stream stream);
+
+/* ------------------------------------------------------------------------ */
+/* Norms (replace Kernels::RMSNorm / ResidualRMSNorm inference_kernel_wrapper, */
+/* rms_norm_kernels.h:50-54, residual_rms_norm_kernels.h:53-59)              */
+/* ------------------------------------------------------------------------ */
+ffmi_status ffmi_rmsnorm(const void *x, const void *w, void *out, int T, int H,
+                         float eps, ffmi_stream stream);
+ffmi_status ffmi_residual_rmsnorm(const void *x1, const void *x2, const void *w,
+                                  void *residual_out, void *out, int T, int H,
+                                  float eps, ffmi_stream stream);
+
+/* ------------------------------------------------------------------------ */
+/* Tensor-parallel all-reduce (replaces Kernels::AllReduce::                 */
+/* inference_kernel_wrapper, allreduce_kernels.h:28-31 / .cu:53-75)          */
+/* ------------------------------------------------------------------------ */
+typedef struct ffmi_comm ffmi_comm;
+#define FFMI_UNIQUE_ID_BYTES 128
+ffmi_status ffmi_comm_unique_id(void *id_out /* FFMI_UNIQUE_ID_BYTES */);
+ffmi_status ffmi_comm_create(const void *id, int nranks, int rank, ffmi_comm **out);
+void ffmi_comm_destroy(ffmi_comm *c);
+ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
+                           int dtype, ffmi_stream stream);
+
+/* ------------------------------------------------------------------------ */
+/* Auxiliary ops on the LLaMA greedy path                                    */
+/* ------------------------------------------------------------------------ */
+/* embed_forward_no_aggr (embedding_kernels.cu:233-244): ids from the batch */
+ffmi_status ffmi_embedding(const ffmi_batch_dev *b, const void *table, void *out,
+                           int H, ffmi_stream stream);
+/* SigmoidSiluMulti standalone (sigmoid_silu_multi.cu:37-47) */
+ffmi_status ffmi_silu_mul(const void *a, const void *b, void *out, size_t n,
+                          ffmi_stream stream);
+/* softmax (fp16 output, softmax.cu:262-288) + ArgMax (argmax.cu:62-100):
+ * ids[t] = lowest index of max fp16(softmax(logits[t]))               */
+ffmi_status ffmi_argmax(const void *logits, int T, int V, int32_t *ids,
+                        float *probs, ffmi_stream stream);
+/* softmax + ArgTopK (arg_topk.cu:339-448), k <= 4, sorted, lower index on ties */
+ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, int32_t *ids,
+                          float *probs, ffmi_stream stream);
+/* seeded synthetic weights, identical to oracle/orc_gen_weight then fp16 */
+ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *name,
+                             uint64_t seed, int kind, ffmi_stream stream);
+
+/* ------------------------------------------------------------------------ */
+/* Serving runtime (C++ host side above the kernels; RequestManager API)     */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+  int num_layers, vocab_size, num_heads, num_kv_heads, hidden, intermediate;
+  float rms_eps, rope_theta;
+} ffmi_llama_config;
+
+typedef enum {
+  FFMI_MODEL_INC = 0,  /* INC_DECODING_MODE  */
+  FFMI_MODEL_BEAM = 1, /* BEAM_SEARCH_MODE (SSM) */
+  FFMI_MODEL_TREE = 2  /* TREE_VERIFY_MODE (LLM) */
+} ffmi_model_mode;
+
+typedef struct {
+  int mode;                  /* ffmi_model_mode                                */
+  int tp_rank, tp_size;      /* tensor parallelism (heads / FFN columns)       */
+  ffmi_comm *comm;           /* RCCL communicator (NULL when tp_size == 1)      */
+  int max_requests;          /* max_requests_per_batch                         */
+  int max_tokens;            /* max tokens per batch (verify capacity for TREE) */
+  int max_seq_len;           /* max_sequence_length                            */
+  int max_tree_tokens;       /* max_spec_tree_token_num                        */
+  uint64_t weight_seed;      /* synthetic weights (orc_gen_weight spec)        */
+  int use_graphs;            /* capture per-shape hipGraphs (0/1)              */
+} ffmi_model_opts;
+
+typedef struct ffmi_model ffmi_model;
+ffmi_status ffmi_model_create(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
+                              ffmi_model **out);
+void ffmi_model_destroy(ffmi_model *m);
+/* Per-op device timing with HIP events on the model's stream (the
+ * reference's --profiling, model.cc:4548-4550).  level 0: off; 1: sampled
+ * (layers 0 and L/2, steps with <= 256 tokens); 2: every op of every step. */
+typedef struct {
+  char name[32];
+  long launches;
+  double total_ms;
+  double bytes; /* algorithmic bytes (weights + activations read/written)  */
+  double flops;
+} ffmi_op_stat;
+ffmi_status ffmi_model_set_profiling(ffmi_model *m, int level);
+int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap);
+/* select the HIP device of the calling thread (one process per GPU) */
+ffmi_status ffmi_set_device(int device);
+
+typedef struct ffmi_rm ffmi_rm;
+typedef struct {
+  int max_requests_per_batch;
+  int max_tokens_per_batch;
+  int max_spec_tree_token_num;
+  int max_sequence_length;
+  int bos_token_id;        /* <0: none                                       */
+  const int *eos_token_ids;
+  int num_eos;
+  const int *spec_tree_width; /* push_spec_infer_tree_width sequence         */
+  int num_tree_width;
+  int verbose;
+} ffmi_rm_config;
+
+ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out);
+void ffmi_rm_destroy(ffmi_rm *rm);
+ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm);
+/* Request: prompt token ids (BOS is prepended when bos_token_id >= 0 and
+ * add_special_tokens), max_length / max_new_tokens as in Request
+ * (request_manager.cc:334-441).  Returns guid (> 0) or 0 on rejection. */
+int64_t ffmi_rm_register_request(ffmi_rm *rm, const int *prompt, int n_prompt,
+                                 int max_length, int max_new_tokens,
+                                 int add_special_tokens);
+/* Run the serve loop until every registered request completes
+ * (serve_incr_decoding / serve_spec_infer, request_manager.cc:3012-3173). */
+ffmi_status ffmi_rm_serve_incr_decoding(ffmi_rm *rm, ffmi_model *llm);
+ffmi_status ffmi_rm_serve_spec_infer(ffmi_rm *rm, ffmi_model *llm);
+/* GenerationResult.output_tokens; returns count (or needed size) */
+int ffmi_rm_get_output(ffmi_rm *rm, int64_t guid, int *tokens, int cap);
+typedef struct {
+  int llm_decoding_steps, ssm_decoding_steps;
+  double start_us, finish_us, registration_us, first_token_us;
+  int input_len, output_len;
+} ffmi_profile;
+ffmi_status ffmi_rm_get_profile(ffmi_rm *rm, int64_t guid, ffmi_profile *p);
+/* aggregate counters of the last serve call */
+typedef struct {
+  long llm_steps, ssm_steps, tokens_committed, tree_tokens_verified;
+  double wall_us;
+} ffmi_serve_stats;
+ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
+
+/* Scheduler test double (no GPU): a deterministic hash "model" whose next
+ * token is a function of the exact token context each query sees through the
+ * KV-slot / bitmask rules, so the RequestManager's batching, tree build,
+ * verification and commit lists can be checked on CPU.  TEST USE ONLY. */
+ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
+                                        int max_seq, int max_tree, uint64_t salt,
+                                        int disagree_pct, ffmi_model **out);
+
+const char *ffmi_status_str(ffmi_status s);
+const char *ffmi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FFMI_H_ */

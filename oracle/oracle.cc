@@ -1,0 +1,561 @@
+// oracle.cc -- CPU restatement of the SpecInfer hot path (TEST INFRASTRUCTURE).
+//
+// See oracle.h for the contract.  Nothing in the product path (libffmi.so)
+// links or calls this file.  Reference citations are file:line into
+// hugolatendresse/FlexFlow @ 2025-01-17.
+#include "oracle.h"
+
+#include <math.h>
+#include <omp.h>
+#include <string.h>
+
+#include <algorithm>
+#include <string>
+#include <vector>
+
+// ----------------------------------------------------------------------------
+// fp16 <-> fp32, round to nearest even (bit exact, subnormals kept)
+// ----------------------------------------------------------------------------
+extern "C" uint16_t orc_f2h(float f) {
+  uint32_t x;
+  memcpy(&x, &f, 4);
+  uint32_t sign = (x >> 16) & 0x8000u;
+  uint32_t a = x & 0x7fffffffu;
+  if (a >= 0x7f800000u) {  // inf / nan
+    return (uint16_t)(sign | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u));
+  }
+  if (a >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // >= 65520 -> inf
+  if (a < 0x38800000u) {                                    // half subnormal
+    float af;
+    memcpy(&af, &a, 4);
+    float r = rintf(af * 16777216.0f);  // exact scale by 2^24, RNE
+    return (uint16_t)(sign | (uint32_t)r);
+  }
+  uint32_t mant = a & 0x7fffffu;
+  uint32_t e = (a >> 23) - 112u;  // rebias 127 -> 15
+  uint32_t h = (e << 10) | (mant >> 13);
+  uint32_t rem = mant & 0x1fffu;
+  if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) h++;
+  return (uint16_t)(sign | h);
+}
+
+extern "C" float orc_h2f(uint16_t h) {
+  uint32_t sign = ((uint32_t)h & 0x8000u) << 16;
+  uint32_t e = (h >> 10) & 0x1fu;
+  uint32_t m = h & 0x3ffu;
+  uint32_t x;
+  if (e == 0) {
+    float v = (float)m * (1.0f / 16777216.0f);
+    return sign ? -v : v;
+  } else if (e == 31) {
+    x = sign | 0x7f800000u | (m << 13);
+  } else {
+    x = sign | ((e + 112u) << 23) | (m << 13);
+  }
+  float f;
+  memcpy(&f, &x, 4);
+  return f;
+}
+
+extern "C" float orc_round16(float f) { return orc_h2f(orc_f2h(f)); }
+
+static inline float R(float v, int fp16) { return fp16 ? orc_round16(v) : v; }
+
+// ----------------------------------------------------------------------------
+// Synthetic weights: counter-based splitmix64 keyed by the tensor name.
+// The GPU generator (flexflow_amd/csrc/kernels/weights.hip) implements the
+// identical spec, so oracle and GPU hold bit-identical weights.
+// ----------------------------------------------------------------------------
+static uint64_t fnv1a64(const char *s) {
+  uint64_t h = 1469598103934665603ull;
+  for (; *s; ++s) {
+    h ^= (uint8_t)*s;
+    h *= 1099511628211ull;
+  }
+  return h;
+}
+
+static inline uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+extern "C" void orc_gen_weight(const char *name, uint64_t seed, int kind,
+                               size_t n, float *out) {
+  const uint64_t key = seed ^ fnv1a64(name);
+  const float center = kind == 1 ? 1.0f : 0.0f;
+  const float amp = kind == 1 ? 0.1f : 0.034641016f;  // 0.02*sqrt(3)
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) {
+    uint64_t x = splitmix64(key + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    float u = (float)(x >> 40) * (1.0f / 16777216.0f);
+    volatile float t = 2.0f * u - 1.0f;  // exact
+    volatile float p = t * amp;           // one rounding
+    out[i] = center + p;                  // one rounding
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Kernel-level restatements
+// ----------------------------------------------------------------------------
+
+// Fixed-order fp32 dot: 8 interleaved partial sums combined pairwise.
+static inline float dot8(const float *a, const float *b, int K) {
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int k = 0;
+  for (; k + 8 <= K; k += 8)
+    for (int j = 0; j < 8; ++j) s[j] += a[k + j] * b[k + j];
+  for (; k < K; ++k) s[k & 7] += a[k] * b[k];
+  return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+// linear_kernels.cu:450-582 (cublasGemmEx OP_T/OP_N, out = in . W^T).
+extern "C" void orc_linear(const float *X, const float *W, float *Y, int T,
+                           int N, int K, int fp16) {
+#pragma omp parallel for schedule(static)
+  for (int n = 0; n < N; ++n) {
+    const float *w = W + (size_t)n * K;
+    for (int t = 0; t < T; ++t) Y[(size_t)t * N + n] = R(dot8(X + (size_t)t * K, w, K), fp16);
+  }
+}
+
+static void rms_core(const float *x, const float *w, float *out, int H,
+                     float eps, int fp16) {
+  double ss = 0.0;
+  for (int j = 0; j < H; ++j) ss += (double)x[j] * (double)x[j];
+  float sum = (float)ss;
+  // rms stored as T (rms_norm_kernels.cu:114)
+  float rms = R(1.0f / sqrtf(sum / (float)H + eps), fp16);
+  for (int j = 0; j < H; ++j) {
+    float y = R(x[j] * rms, fp16);  // Y = X * rms (half)
+    out[j] = R(y * w[j], fp16);     // out = Y * w (half)
+  }
+}
+
+// rms_norm_kernels.cu:97-124
+extern "C" void orc_rmsnorm(const float *X, const float *w, float *out, int T,
+                            int H, float eps, int fp16) {
+  for (int t = 0; t < T; ++t)
+    rms_core(X + (size_t)t * H, w, out + (size_t)t * H, H, eps, fp16);
+}
+
+// residual_rms_norm_kernels.cu:98-131: X_out = X1 + X2 (half), then norm
+extern "C" void orc_residual_rmsnorm(const float *X1, const float *X2,
+                                     const float *w, float *res_out, float *out,
+                                     int T, int H, float eps, int fp16) {
+  for (int t = 0; t < T; ++t) {
+    const float *a = X1 + (size_t)t * H;
+    const float *b = X2 + (size_t)t * H;
+    float *r = res_out + (size_t)t * H;
+    for (int j = 0; j < H; ++j) r[j] = R((float)((double)a[j] + (double)b[j]), fp16);
+    rms_core(r, w, out + (size_t)t * H, H, eps, fp16);
+  }
+}
+
+// sigmoid_silu_multi.cu:37-47: out = a * T(sigmoid(a)) * b, left to right
+extern "C" void orc_silu_mul(const float *A, const float *B, float *out,
+                             size_t n, int fp16) {
+#pragma omp parallel for schedule(static)
+  for (long i = 0; i < (long)n; ++i) {
+    float a = A[i];
+    float sg = 1.0f / (1.0f + expf(-a));
+    float t = R(a * R(sg, fp16), fp16);
+    out[i] = R(t * B[i], fp16);
+  }
+}
+
+// RoPE table: freq = pos * (1.0 / pow(theta, 2i/d)) with the reference's
+// float/double mix (inc_multihead_self_attention.cu:701-703), cos/sin in f32.
+extern "C" void orc_rope_table(float *tab, int max_pos, int d, float theta) {
+  const int h = d / 2;
+  std::vector<double> inv(h);
+  for (int i = 0; i < h; ++i) {
+    float ex = (float)2 * (float)i / (float)d;
+    inv[i] = 1.0 / (double)powf(theta, ex);
+  }
+  for (int p = 0; p < max_pos; ++p)
+    for (int i = 0; i < h; ++i) {
+      float freq = (float)((double)p * inv[i]);
+      tab[((size_t)p * h + i) * 2 + 0] = cosf(freq);
+      tab[((size_t)p * h + i) * 2 + 1] = sinf(freq);
+    }
+}
+
+// apply_rotary_embedding_hf (inc_multihead_self_attention.cu:664-738):
+// pair (i, i + d/2), complex multiply in f32, store as T.
+static void rope_apply(float *x, int d, const float *cs) {
+  const int h = d / 2;
+  for (int i = 0; i < h; ++i) {
+    float c = cs[2 * i], s = cs[2 * i + 1];
+    float a = x[i], b = x[i + h];
+    float ac = a * c, bs = b * s, as = a * s, bc = b * c;
+    x[i] = ac - bs;
+    x[i + h] = as + bc;
+  }
+}
+
+extern "C" void orc_rope_head(float *x, int d, int pos, float theta, int fp16) {
+  std::vector<float> tab((size_t)(pos + 1) * d);
+  orc_rope_table(tab.data(), pos + 1, d, theta);
+  rope_apply(x, d, tab.data() + (size_t)pos * d);
+  for (int i = 0; i < d; ++i) x[i] = R(x[i], fp16);
+}
+
+// compute_attention_kernel_generation_kernel (inc_...cu:372-623) and the
+// masked variants (tree_inc...cu:135-333, spec_inc...cu:130-300).
+extern "C" void orc_attention_row(const float *q, const float *K,
+                                  const float *V, const uint8_t *visible,
+                                  int n_keys, int d, float scale, float *out,
+                                  int fp16) {
+  std::vector<float> p(n_keys > 0 ? n_keys : 1);
+  float mx = -3.402823466e38f;
+  for (int j = 0; j < n_keys; ++j) {
+    if (!visible[j]) continue;
+    const float *k = K + (size_t)j * d;
+    float acc = 0.f;
+    for (int i = 0; i < d; ++i) acc += q[i] * k[i];
+    p[j] = scale * acc;
+    mx = std::max(mx, p[j]);
+  }
+  double sum = 0.0;
+  for (int j = 0; j < n_keys; ++j) {
+    p[j] = visible[j] ? expf(p[j] - mx) : 0.f;
+    sum += p[j];
+  }
+  float inv = 1.0f / ((float)sum + 1e-6f);
+  for (int i = 0; i < d; ++i) out[i] = 0.f;
+  for (int j = 0; j < n_keys; ++j) {
+    if (!visible[j]) continue;
+    float w = p[j] * inv;
+    const float *v = V + (size_t)j * d;
+    for (int i = 0; i < d; ++i) out[i] += w * v[i];
+  }
+  for (int i = 0; i < d; ++i) out[i] = R(out[i], fp16);
+}
+
+// softmax over the vocab (softmax.cu:262-288; output stored as T), then the
+// greedy pick (argmax.cu:62-100: first maximum).
+static void softmax_row(const float *x, int V, int fp16, float *p) {
+  float mx = -3.402823466e38f;
+  for (int i = 0; i < V; ++i) mx = std::max(mx, x[i]);
+  double sum = 0.0;
+  for (int i = 0; i < V; ++i) {
+    p[i] = expf(x[i] - mx);
+    sum += p[i];
+  }
+  float s = (float)sum;
+  for (int i = 0; i < V; ++i) p[i] = R(p[i] / s, fp16);
+}
+
+extern "C" void orc_softmax_argmax(const float *logits, int T, int V, int fp16,
+                                   int *out_ids, float *out_prob) {
+  std::vector<float> p(V);
+  for (int t = 0; t < T; ++t) {
+    softmax_row(logits + (size_t)t * V, V, fp16, p.data());
+    int best = 0;
+    for (int i = 1; i < V; ++i)
+      if (p[i] > p[best]) best = i;
+    out_ids[t] = best;
+    if (out_prob) out_prob[t] = p[best];
+  }
+}
+
+// arg_topk.cu:208-330: min-heap preferring higher index for eviction ->
+// equal values keep the lower index; output sorted by value desc, index asc.
+extern "C" void orc_softmax_topk(const float *logits, int T, int V, int k,
+                                 int fp16, int *out_ids, float *out_probs) {
+  std::vector<float> p(V);
+  std::vector<int> idx(V);
+  for (int t = 0; t < T; ++t) {
+    softmax_row(logits + (size_t)t * V, V, fp16, p.data());
+    for (int i = 0; i < V; ++i) idx[i] = i;
+    std::partial_sort(idx.begin(), idx.begin() + k, idx.end(), [&](int a, int b) {
+      return p[a] > p[b] || (p[a] == p[b] && a < b);
+    });
+    for (int j = 0; j < k; ++j) {
+      out_ids[(size_t)t * k + j] = idx[j];
+      if (out_probs) out_probs[(size_t)t * k + j] = p[idx[j]];
+    }
+  }
+}
+
+// ----------------------------------------------------------------------------
+// Model-level restatement: LLaMA graph of inference/models/llama.cc:23-317
+// (embedding -> [rms | residual_rms] -> qkv -> IncMHA -> o -> residual_rms
+//  -> gate/up -> silu_mul -> down) x L -> residual_rms "norm" -> lm_head.
+// ----------------------------------------------------------------------------
+struct orc_model {
+  orc_config c;
+  int fp16;
+  int max_requests, max_seq;
+  int d;
+  std::vector<float> emb, lm, final_norm;
+  struct Layer {
+    std::vector<float> in_norm, post_norm, wq, wk, wv, wo, wg, wu, wd;
+  };
+  std::vector<Layer> layers;
+  std::vector<float> kc, vc;  // [req][layer][pos][H]
+  std::vector<float> rope;    // [max_seq][d/2][2]
+  std::vector<std::vector<float>> hidden;  // debug: per-layer output of last call
+};
+
+static void gen(std::vector<float> &dst, const std::string &name, uint64_t seed,
+                int kind, size_t n, int fp16) {
+  dst.resize(n);
+  orc_gen_weight(name.c_str(), seed, kind, n, dst.data());
+  if (fp16)
+    for (auto &v : dst) v = orc_round16(v);
+}
+
+extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
+                                       int fp16, int max_requests, int max_seq) {
+  if (cfg->num_kv_heads != cfg->num_heads) return nullptr;  // MHA only
+  orc_model *m = new orc_model();
+  m->c = *cfg;
+  m->fp16 = fp16;
+  m->max_requests = max_requests;
+  m->max_seq = max_seq;
+  m->d = cfg->hidden / cfg->num_heads;
+  const size_t H = cfg->hidden, F = cfg->intermediate, Vv = cfg->vocab_size;
+  gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16);
+  gen(m->lm, "lm_head.weight", seed, 0, Vv * H, fp16);
+  gen(m->final_norm, "model.norm.weight", seed, 1, H, fp16);
+  m->layers.resize(cfg->num_layers);
+  for (int l = 0; l < cfg->num_layers; ++l) {
+    std::string p = "model.layers." + std::to_string(l) + ".";
+    auto &L = m->layers[l];
+    gen(L.in_norm, p + "input_layernorm.weight", seed, 1, H, fp16);
+    gen(L.post_norm, p + "post_attention_layernorm.weight", seed, 1, H, fp16);
+    gen(L.wq, p + "self_attn.q_proj.weight", seed, 0, H * H, fp16);
+    gen(L.wk, p + "self_attn.k_proj.weight", seed, 0, H * H, fp16);
+    gen(L.wv, p + "self_attn.v_proj.weight", seed, 0, H * H, fp16);
+    gen(L.wo, p + "self_attn.o_proj.weight", seed, 0, H * H, fp16);
+    gen(L.wg, p + "mlp.gate_proj.weight", seed, 0, F * H, fp16);
+    gen(L.wu, p + "mlp.up_proj.weight", seed, 0, F * H, fp16);
+    gen(L.wd, p + "mlp.down_proj.weight", seed, 0, H * F, fp16);
+  }
+  m->kc.assign((size_t)max_requests * cfg->num_layers * max_seq * H, 0.f);
+  m->vc.assign((size_t)max_requests * cfg->num_layers * max_seq * H, 0.f);
+  m->rope.resize((size_t)max_seq * m->d);
+  orc_rope_table(m->rope.data(), max_seq, m->d, cfg->rope_theta);
+  m->hidden.resize(cfg->num_layers + 1);
+  return m;
+}
+
+extern "C" void orc_model_destroy(orc_model *m) { delete m; }
+
+extern "C" void orc_model_reset(orc_model *m, int req) {
+  (void)m;
+  (void)req;  // cache rows are overwritten position by position
+}
+
+extern "C" long orc_model_weight(orc_model *m, const char *name, float *out) {
+  std::string n(name);
+  const std::vector<float> *src = nullptr;
+  if (n == "model.embed_tokens.weight") src = &m->emb;
+  else if (n == "lm_head.weight") src = &m->lm;
+  else if (n == "model.norm.weight") src = &m->final_norm;
+  else if (n.rfind("model.layers.", 0) == 0) {
+    int l = atoi(n.c_str() + 13);
+    if (l < 0 || l >= m->c.num_layers) return -1;
+    auto &L = m->layers[l];
+    std::string rest = n.substr(n.find('.', 13) + 1);
+    if (rest == "input_layernorm.weight") src = &L.in_norm;
+    else if (rest == "post_attention_layernorm.weight") src = &L.post_norm;
+    else if (rest == "self_attn.q_proj.weight") src = &L.wq;
+    else if (rest == "self_attn.k_proj.weight") src = &L.wk;
+    else if (rest == "self_attn.v_proj.weight") src = &L.wv;
+    else if (rest == "self_attn.o_proj.weight") src = &L.wo;
+    else if (rest == "mlp.gate_proj.weight") src = &L.wg;
+    else if (rest == "mlp.up_proj.weight") src = &L.wu;
+    else if (rest == "mlp.down_proj.weight") src = &L.wd;
+  }
+  if (!src) return -1;
+  if (out) memcpy(out, src->data(), src->size() * sizeof(float));
+  return (long)src->size();
+}
+
+extern "C" int orc_model_forward(orc_model *m, int req, const int *tokens, int T,
+                                 int start_pos, float *logits) {
+  const orc_config &c = m->c;
+  const int H = c.hidden, F = c.intermediate, d = m->d, nh = c.num_heads;
+  const int fp16 = m->fp16;
+  if (req < 0 || req >= m->max_requests || start_pos + T > m->max_seq) return -1;
+  std::vector<float> x((size_t)T * H), h((size_t)T * H), res((size_t)T * H);
+  std::vector<float> q((size_t)T * H), k((size_t)T * H), v((size_t)T * H);
+  std::vector<float> att((size_t)T * H), o((size_t)T * H), mlp((size_t)T * H);
+  std::vector<float> g((size_t)T * F), u((size_t)T * F), a((size_t)T * F);
+  for (int t = 0; t < T; ++t)
+    memcpy(&x[(size_t)t * H], &m->emb[(size_t)tokens[t] * H], H * sizeof(float));
+  const float scale = 1.0f / sqrtf((float)d);
+  for (int l = 0; l < c.num_layers; ++l) {
+    auto &L = m->layers[l];
+    if (l == 0) {
+      res = x;
+      orc_rmsnorm(res.data(), L.in_norm.data(), h.data(), T, H, c.rms_eps, fp16);
+    } else {
+      std::vector<float> r2((size_t)T * H);
+      orc_residual_rmsnorm(res.data(), mlp.data(), L.in_norm.data(), r2.data(),
+                           h.data(), T, H, c.rms_eps, fp16);
+      res.swap(r2);
+    }
+    orc_linear(h.data(), L.wq.data(), q.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wk.data(), k.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wv.data(), v.data(), T, H, H, fp16);
+    float *kc = &m->kc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
+    float *vc = &m->vc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
+    for (int t = 0; t < T; ++t) {
+      int pos = start_pos + t;
+      for (int hd = 0; hd < nh; ++hd) {
+        float *qh = &q[(size_t)t * H + hd * d];
+        float *kh = &k[(size_t)t * H + hd * d];
+        rope_apply(qh, d, &m->rope[(size_t)pos * d]);
+        rope_apply(kh, d, &m->rope[(size_t)pos * d]);
+        for (int i = 0; i < d; ++i) {
+          qh[i] = R(qh[i], fp16);
+          kh[i] = R(kh[i], fp16);
+        }
+      }
+      memcpy(kc + (size_t)pos * H, &k[(size_t)t * H], H * sizeof(float));
+      memcpy(vc + (size_t)pos * H, &v[(size_t)t * H], H * sizeof(float));
+    }
+    const int nk = start_pos + T;
+#pragma omp parallel
+    {
+      std::vector<float> Kh((size_t)nk * d), Vh((size_t)nk * d);
+      std::vector<uint8_t> vis(nk);
+#pragma omp for schedule(static)
+      for (int hd = 0; hd < nh; ++hd) {
+        for (int j = 0; j < nk; ++j) {
+          memcpy(&Kh[(size_t)j * d], kc + (size_t)j * H + hd * d, d * sizeof(float));
+          memcpy(&Vh[(size_t)j * d], vc + (size_t)j * H + hd * d, d * sizeof(float));
+        }
+        for (int t = 0; t < T; ++t) {
+          int pos = start_pos + t;
+          for (int j = 0; j < nk; ++j) vis[j] = j <= pos;
+          orc_attention_row(&q[(size_t)t * H + hd * d], Kh.data(), Vh.data(),
+                            vis.data(), nk, d, scale, &att[(size_t)t * H + hd * d], fp16);
+        }
+      }
+    }
+    orc_linear(att.data(), L.wo.data(), o.data(), T, H, H, fp16);
+    {
+      std::vector<float> r2((size_t)T * H);
+      orc_residual_rmsnorm(res.data(), o.data(), L.post_norm.data(), r2.data(),
+                           h.data(), T, H, c.rms_eps, fp16);
+      res.swap(r2);
+    }
+    orc_linear(h.data(), L.wg.data(), g.data(), T, F, H, fp16);
+    orc_linear(h.data(), L.wu.data(), u.data(), T, F, H, fp16);
+    orc_silu_mul(g.data(), u.data(), a.data(), (size_t)T * F, fp16);
+    orc_linear(a.data(), L.wd.data(), mlp.data(), T, H, F, fp16);
+    // debug: residual stream entering the next layer (= res + mlp)
+    auto &dbg = m->hidden[l];
+    dbg.resize((size_t)T * H);
+    for (size_t i = 0; i < dbg.size(); ++i) dbg[i] = R(res[i] + mlp[i], fp16);
+  }
+  std::vector<float> r2((size_t)T * H);
+  orc_residual_rmsnorm(res.data(), mlp.data(), m->final_norm.data(), r2.data(),
+                       h.data(), T, H, c.rms_eps, fp16);
+  m->hidden[c.num_layers] = h;
+  if (logits)
+    orc_linear(h.data(), m->lm.data(), logits, T, c.vocab_size, H, fp16);
+  return 0;
+}
+
+extern "C" int orc_model_decode_batch(orc_model *m, const int *reqs, const int *tokens,
+                                      const int *pos, int T, float *logits) {
+  const orc_config &c = m->c;
+  const int H = c.hidden, F = c.intermediate, d = m->d, nh = c.num_heads;
+  const int fp16 = m->fp16;
+  for (int t = 0; t < T; ++t)
+    if (reqs[t] < 0 || reqs[t] >= m->max_requests || pos[t] >= m->max_seq) return -1;
+  std::vector<float> res((size_t)T * H), h((size_t)T * H), r2((size_t)T * H);
+  std::vector<float> q((size_t)T * H), k((size_t)T * H), v((size_t)T * H);
+  std::vector<float> att((size_t)T * H), o((size_t)T * H), mlp((size_t)T * H);
+  std::vector<float> g((size_t)T * F), u((size_t)T * F), a((size_t)T * F);
+  for (int t = 0; t < T; ++t)
+    memcpy(&res[(size_t)t * H], &m->emb[(size_t)tokens[t] * H], H * sizeof(float));
+  const float scale = 1.0f / sqrtf((float)d);
+  for (int l = 0; l < c.num_layers; ++l) {
+    auto &L = m->layers[l];
+    if (l == 0) {
+      orc_rmsnorm(res.data(), L.in_norm.data(), h.data(), T, H, c.rms_eps, fp16);
+    } else {
+      orc_residual_rmsnorm(res.data(), mlp.data(), L.in_norm.data(), r2.data(), h.data(), T,
+                           H, c.rms_eps, fp16);
+      res.swap(r2);
+    }
+    orc_linear(h.data(), L.wq.data(), q.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wk.data(), k.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wv.data(), v.data(), T, H, H, fp16);
+#pragma omp parallel for schedule(static)
+    for (int t = 0; t < T; ++t) {
+      const int req = reqs[t], p = pos[t];
+      float *kc = &m->kc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
+      float *vc = &m->vc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
+      for (int hd = 0; hd < nh; ++hd) {
+        float *qh = &q[(size_t)t * H + hd * d];
+        float *kh = &k[(size_t)t * H + hd * d];
+        rope_apply(qh, d, &m->rope[(size_t)p * d]);
+        rope_apply(kh, d, &m->rope[(size_t)p * d]);
+        for (int i = 0; i < d; ++i) {
+          qh[i] = R(qh[i], fp16);
+          kh[i] = R(kh[i], fp16);
+        }
+      }
+      memcpy(kc + (size_t)p * H, &k[(size_t)t * H], H * sizeof(float));
+      memcpy(vc + (size_t)p * H, &v[(size_t)t * H], H * sizeof(float));
+      std::vector<float> Kh((size_t)(p + 1) * d), Vh((size_t)(p + 1) * d);
+      std::vector<uint8_t> vis(p + 1, 1);
+      for (int hd = 0; hd < nh; ++hd) {
+        for (int j = 0; j <= p; ++j) {
+          memcpy(&Kh[(size_t)j * d], kc + (size_t)j * H + hd * d, d * sizeof(float));
+          memcpy(&Vh[(size_t)j * d], vc + (size_t)j * H + hd * d, d * sizeof(float));
+        }
+        orc_attention_row(&q[(size_t)t * H + hd * d], Kh.data(), Vh.data(), vis.data(), p + 1,
+                          d, scale, &att[(size_t)t * H + hd * d], fp16);
+      }
+    }
+    orc_linear(att.data(), L.wo.data(), o.data(), T, H, H, fp16);
+    orc_residual_rmsnorm(res.data(), o.data(), L.post_norm.data(), r2.data(), h.data(), T, H,
+                         c.rms_eps, fp16);
+    res.swap(r2);
+    orc_linear(h.data(), L.wg.data(), g.data(), T, F, H, fp16);
+    orc_linear(h.data(), L.wu.data(), u.data(), T, F, H, fp16);
+    orc_silu_mul(g.data(), u.data(), a.data(), (size_t)T * F, fp16);
+    orc_linear(a.data(), L.wd.data(), mlp.data(), T, H, F, fp16);
+  }
+  orc_residual_rmsnorm(res.data(), mlp.data(), m->final_norm.data(), r2.data(), h.data(), T, H,
+                       c.rms_eps, fp16);
+  if (logits) orc_linear(h.data(), m->lm.data(), logits, T, c.vocab_size, H, fp16);
+  return 0;
+}
+
+extern "C" int orc_model_get_hidden(orc_model *m, int layer, float *out) {
+  if (layer < 0 || layer > m->c.num_layers) return -1;
+  auto &v = m->hidden[layer];
+  memcpy(out, v.data(), v.size() * sizeof(float));
+  return (int)(v.size() / m->c.hidden);
+}
+
+extern "C" int orc_model_greedy(orc_model *m, int req, const int *prompt,
+                                int n_prompt, int n_new, int *out_tokens) {
+  const int V = m->c.vocab_size;
+  std::vector<float> logits((size_t)n_prompt * V);
+  if (orc_model_forward(m, req, prompt, n_prompt, 0, logits.data())) return -1;
+  int tok;
+  orc_softmax_argmax(&logits[(size_t)(n_prompt - 1) * V], 1, V, m->fp16, &tok, nullptr);
+  int pos = n_prompt;
+  for (int i = 0; i < n_new; ++i) {
+    out_tokens[i] = tok;
+    if (i + 1 == n_new) break;
+    if (orc_model_forward(m, req, &tok, 1, pos, logits.data())) return -1;
+    ++pos;
+    orc_softmax_argmax(logits.data(), 1, V, m->fp16, &tok, nullptr);
+  }
+  return 0;
+}
+
+extern "C" int orc_num_threads(void) { return omp_get_max_threads(); }

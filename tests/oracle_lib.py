@@ -1,0 +1,228 @@
+"""ctypes binding of oracle/liboracle.so -- TEST INFRASTRUCTURE ONLY.
+
+Used by tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg as
+the checker / CPU baseline.  Never imported by flexflow_amd/.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i32p = ctypes.POINTER(ctypes.c_int)
+_u8p = ctypes.POINTER(ctypes.c_uint8)
+
+
+class OrcConfig(ctypes.Structure):
+    _fields_ = [("num_layers", ctypes.c_int), ("vocab_size", ctypes.c_int),
+                ("num_heads", ctypes.c_int), ("num_kv_heads", ctypes.c_int),
+                ("hidden", ctypes.c_int), ("intermediate", ctypes.c_int),
+                ("rms_eps", ctypes.c_float), ("rope_theta", ctypes.c_float)]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            import subprocess
+            subprocess.check_call(["make", "-C", os.path.dirname(LIB_PATH)])
+        L = ctypes.CDLL(LIB_PATH)
+        L.orc_f2h.restype = ctypes.c_uint16
+        L.orc_f2h.argtypes = [ctypes.c_float]
+        L.orc_h2f.restype = ctypes.c_float
+        L.orc_h2f.argtypes = [ctypes.c_uint16]
+        L.orc_gen_weight.argtypes = [ctypes.c_char_p, ctypes.c_uint64, ctypes.c_int,
+                                     ctypes.c_size_t, _f32p]
+        L.orc_linear.argtypes = [_f32p, _f32p, _f32p] + [ctypes.c_int] * 4
+        L.orc_rmsnorm.argtypes = [_f32p, _f32p, _f32p, ctypes.c_int, ctypes.c_int,
+                                  ctypes.c_float, ctypes.c_int]
+        L.orc_residual_rmsnorm.argtypes = [_f32p] * 5 + [ctypes.c_int, ctypes.c_int,
+                                                         ctypes.c_float, ctypes.c_int]
+        L.orc_silu_mul.argtypes = [_f32p, _f32p, _f32p, ctypes.c_size_t, ctypes.c_int]
+        L.orc_rope_table.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float]
+        L.orc_rope_head.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                    ctypes.c_int]
+        L.orc_attention_row.argtypes = [_f32p, _f32p, _f32p, _u8p, ctypes.c_int,
+                                        ctypes.c_int, ctypes.c_float, _f32p, ctypes.c_int]
+        L.orc_softmax_argmax.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         _i32p, _f32p]
+        L.orc_softmax_topk.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                       ctypes.c_int, _i32p, _f32p]
+        L.orc_model_create.restype = ctypes.c_void_p
+        L.orc_model_create.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64,
+                                       ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_model_destroy.argtypes = [ctypes.c_void_p]
+        L.orc_model_forward.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
+                                        ctypes.c_int, ctypes.c_int, _f32p]
+        L.orc_model_decode_batch.argtypes = [ctypes.c_void_p, _i32p, _i32p, _i32p,
+                                             ctypes.c_int, _f32p]
+        L.orc_model_get_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.orc_model_greedy.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
+                                       ctypes.c_int, ctypes.c_int, _i32p]
+        L.orc_model_weight.restype = ctypes.c_long
+        L.orc_model_weight.argtypes = [ctypes.c_void_p, ctypes.c_char_p, _f32p]
+        L.orc_num_threads.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def fp(a):
+    return a.ctypes.data_as(_f32p)
+
+
+def ip(a):
+    return a.ctypes.data_as(_i32p)
+
+
+def round16(x):
+    return np.asarray(x, np.float32).astype(np.float16).astype(np.float32)
+
+
+def gen_weight(name, seed, kind, n):
+    out = np.empty(n, np.float32)
+    lib().orc_gen_weight(name.encode(), seed, kind, n, fp(out))
+    return out
+
+
+def linear(X, W, fp16=1):
+    X = np.ascontiguousarray(X, np.float32)
+    W = np.ascontiguousarray(W, np.float32)
+    T, K = X.shape
+    N = W.shape[0]
+    Y = np.empty((T, N), np.float32)
+    lib().orc_linear(fp(X), fp(W), fp(Y), T, N, K, fp16)
+    return Y
+
+
+def rmsnorm(X, w, eps, fp16=1):
+    X = np.ascontiguousarray(X, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    out = np.empty_like(X)
+    lib().orc_rmsnorm(fp(X), fp(w), fp(out), X.shape[0], X.shape[1], eps, fp16)
+    return out
+
+
+def residual_rmsnorm(X1, X2, w, eps, fp16=1):
+    X1 = np.ascontiguousarray(X1, np.float32)
+    X2 = np.ascontiguousarray(X2, np.float32)
+    w = np.ascontiguousarray(w, np.float32)
+    res = np.empty_like(X1)
+    out = np.empty_like(X1)
+    lib().orc_residual_rmsnorm(fp(X1), fp(X2), fp(w), fp(res), fp(out), X1.shape[0],
+                               X1.shape[1], eps, fp16)
+    return res, out
+
+
+def silu_mul(A, B, fp16=1):
+    A = np.ascontiguousarray(A, np.float32)
+    B = np.ascontiguousarray(B, np.float32)
+    out = np.empty_like(A)
+    lib().orc_silu_mul(fp(A), fp(B), fp(out), A.size, fp16)
+    return out
+
+
+def rope_table(max_pos, d, theta):
+    tab = np.empty(max_pos * d, np.float32)
+    lib().orc_rope_table(fp(tab), max_pos, d, theta)
+    return tab
+
+
+def attention_row(q, K, V, visible, scale, fp16=1):
+    q = np.ascontiguousarray(q, np.float32)
+    K = np.ascontiguousarray(K, np.float32)
+    V = np.ascontiguousarray(V, np.float32)
+    vis = np.ascontiguousarray(visible, np.uint8)
+    d = q.shape[0]
+    out = np.empty(d, np.float32)
+    lib().orc_attention_row(fp(q), fp(K), fp(V), vis.ctypes.data_as(_u8p), K.shape[0], d,
+                            scale, fp(out), fp16)
+    return out
+
+
+def softmax_argmax(logits, fp16=1):
+    logits = np.ascontiguousarray(logits, np.float32)
+    T, V = logits.shape
+    ids = np.empty(T, np.int32)
+    probs = np.empty(T, np.float32)
+    lib().orc_softmax_argmax(fp(logits), T, V, fp16, ip(ids), fp(probs))
+    return ids, probs
+
+
+def softmax_topk(logits, k, fp16=1):
+    logits = np.ascontiguousarray(logits, np.float32)
+    T, V = logits.shape
+    ids = np.empty((T, k), np.int32)
+    probs = np.empty((T, k), np.float32)
+    lib().orc_softmax_topk(fp(logits), T, V, k, fp16, ip(ids), fp(probs))
+    return ids, probs
+
+
+class Model:
+    """Oracle LLaMA (llama.cc restatement), one KV cache row per request."""
+
+    def __init__(self, cfg, seed, fp16=1, max_requests=4, max_seq=512):
+        self.cfg = dict(cfg)
+        c = OrcConfig(cfg["num_layers"], cfg["vocab_size"], cfg["num_heads"],
+                      cfg.get("num_kv_heads", cfg["num_heads"]), cfg["hidden"],
+                      cfg["intermediate"], cfg.get("rms_eps", 1e-6),
+                      cfg.get("rope_theta", 10000.0))
+        self.h = lib().orc_model_create(ctypes.byref(c), seed, fp16, max_requests, max_seq)
+        if not self.h:
+            raise RuntimeError("orc_model_create failed")
+        self.fp16 = fp16
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_model_destroy(self.h)
+            self.h = None
+
+    def forward(self, req, tokens, start_pos):
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        T = tokens.shape[0]
+        logits = np.empty((T, self.cfg["vocab_size"]), np.float32)
+        rc = lib().orc_model_forward(self.h, req, ip(tokens), T, start_pos, fp(logits))
+        assert rc == 0
+        return logits
+
+    def decode_batch(self, reqs, tokens, pos):
+        reqs = np.ascontiguousarray(reqs, np.int32)
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        pos = np.ascontiguousarray(pos, np.int32)
+        T = tokens.shape[0]
+        logits = np.empty((T, self.cfg["vocab_size"]), np.float32)
+        rc = lib().orc_model_decode_batch(self.h, ip(reqs), ip(tokens), ip(pos), T, fp(logits))
+        assert rc == 0
+        return logits
+
+    def hidden(self, layer, T):
+        out = np.empty((T, self.cfg["hidden"]), np.float32)
+        lib().orc_model_get_hidden(self.h, layer, fp(out))
+        return out
+
+    def greedy(self, req, prompt, n_new):
+        prompt = np.ascontiguousarray(prompt, np.int32)
+        out = np.empty(n_new, np.int32)
+        rc = lib().orc_model_greedy(self.h, req, ip(prompt), prompt.shape[0], n_new, ip(out))
+        assert rc == 0
+        return out
+
+    def weight(self, name):
+        n = lib().orc_model_weight(self.h, name.encode(), None)
+        assert n > 0, name
+        out = np.empty(n, np.float32)
+        lib().orc_model_weight(self.h, name.encode(), fp(out))
+        return out
+
+
+def load_golden(tag):
+    path = os.path.join(ROOT, "tests", "golden", f"{tag}.npz")
+    z = np.load(path, allow_pickle=False)
+    cfg = json.loads(str(z["config"]))
+    return cfg, {k: z[k] for k in z.files if k != "config"}

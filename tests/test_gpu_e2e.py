@@ -1,0 +1,123 @@
+"""End-to-end GPU parity: greedy tokens of the MI355X path vs the CPU oracle,
+and the reference's SpecInfer invariant (spec_infer tokens == incr_decoding
+tokens, tests/inference/cpp_inference_tests.sh:183-189).
+
+Token parity rule (fp16 model, fp32 accumulation everywhere, different fp32
+summation order on GPU and CPU): the GPU sequence is teacher-forced through
+the oracle; every GPU token must equal the oracle's greedy pick unless the
+oracle's fp16 softmax probabilities of the two tokens are within 2 fp16 ulp
+(a numerical tie), and >= 90% of tokens must be exact picks.
+"""
+import numpy as np
+import pytest
+
+import flexflow_amd as fa
+import oracle_lib as O
+from hip_util import ulp_diff
+
+pytestmark = pytest.mark.gpu
+
+LLM_CFG = dict(num_layers=2, vocab_size=1000, num_heads=2, num_kv_heads=2, hidden=256,
+               intermediate=512, rms_eps=1e-6, rope_theta=10000.0)
+SSM_CFG = dict(num_layers=1, vocab_size=1000, num_heads=2, num_kv_heads=2, hidden=128,
+               intermediate=256, rms_eps=1e-6, rope_theta=10000.0)
+
+
+def prompts(n, V, lo, hi, seed):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(3, V, size=int(rng.integers(lo, hi))).tolist() for _ in range(n)]
+
+
+def check_tokens_vs_oracle(cfg, seed, seq, n_prompt):
+    """teacher-forced check of seq[n_prompt:] against the oracle."""
+    m = O.Model(cfg, seed, fp16=1, max_requests=1, max_seq=len(seq) + 1)
+    logits = m.forward(0, np.array(seq[:-1], np.int32), 0)
+    gen = seq[n_prompt:]
+    lg = logits[n_prompt - 1:]
+    ids, _ = O.softmax_argmax(lg, fp16=1)
+    exact = 0
+    for t, g in enumerate(gen):
+        if ids[t] == g:
+            exact += 1
+            continue
+        row = lg[t]
+        p = np.exp(row - row.max())
+        p16 = (p / p.sum()).astype(np.float16)
+        assert ulp_diff(p16[g], p16[ids[t]]) <= 2, (t, g, ids[t], float(p16[g]), float(p16[ids[t]]))
+    assert exact >= 0.9 * len(gen), (exact, len(gen))
+    return exact
+
+
+@pytest.mark.parametrize("cfg,seed", [(LLM_CFG, 11), (SSM_CFG, 5)])
+def test_incr_decoding_tokens_match_oracle(cfg, seed):
+    V = cfg["vocab_size"]
+    ps = prompts(5, V, 4, 30, seed)
+    rm = fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=32,
+                           max_sequence_length=128)
+    llm = fa.Model(cfg, "inc", max_requests=4, max_tokens=32, max_seq_len=128, weight_seed=seed)
+    res = fa.generate(rm, llm, ps, max_length=64)
+    for p, r in zip(ps, res):
+        assert len(r.output_tokens) == 64
+        check_tokens_vs_oracle(cfg, seed, r.output_tokens, len(p) + 1)
+
+
+def test_incr_decoding_matches_golden_fixture_model():
+    # the HF-pinned fixture model (oracle fp32 == HF greedy); GPU fp16 vs oracle fp16
+    cfg, g = O.load_golden("tiny_d128")
+    rm = fa.RequestManager(max_requests_per_batch=1, max_tokens_per_batch=16,
+                           max_sequence_length=64)
+    llm = fa.Model(cfg, "inc", max_requests=1, max_tokens=16, max_seq_len=64,
+                   weight_seed=cfg["seed"])
+    prompt = g["prompt"].tolist()
+    res = fa.generate(rm, llm, [prompt[1:]], max_length=len(prompt) + cfg["n_new"])
+    check_tokens_vs_oracle(cfg, cfg["seed"], res[0].output_tokens, len(prompt))
+
+
+def run_spec(ps, max_length, ssm_cfg, ssm_seed, widths=(1, 1, 3), batch=4, max_tokens=64):
+    rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
+                           max_sequence_length=128, spec_tree_width=widths,
+                           max_spec_tree_token_num=23)
+    vt = max_tokens + 23 * batch
+    llm = fa.Model(LLM_CFG, "tree", max_requests=batch, max_tokens=vt, max_seq_len=128,
+                   max_tree_tokens=23, weight_seed=11)
+    ssm = fa.Model(ssm_cfg, "beam", max_requests=batch, max_tokens=vt, max_seq_len=128,
+                   max_tree_tokens=23, weight_seed=ssm_seed)
+    rm.register_ssm_model(ssm)
+    res = fa.generate(rm, llm, ps, max_length=max_length)
+    return res, rm.stats()
+
+
+def run_incr(ps, max_length, batch=4, max_tokens=64):
+    rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
+                           max_sequence_length=128)
+    llm = fa.Model(LLM_CFG, "inc", max_requests=batch, max_tokens=max_tokens, max_seq_len=128,
+                   weight_seed=11)
+    return fa.generate(rm, llm, ps, max_length=max_length), rm.stats()
+
+
+def first_divergence(a, b):
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x != y:
+            return i
+    return min(len(a), len(b))
+
+
+@pytest.mark.parametrize("ssm", ["small", "same"])
+def test_spec_infer_equals_incr_on_gpu(ssm):
+    ps = prompts(4, 1000, 5, 40, 3)
+    inc, s_inc = run_incr(ps, 80)
+    if ssm == "small":
+        spec, s_spec = run_spec(ps, 80, SSM_CFG, 5)
+    else:  # SSM == LLM weights: near-100% acceptance exercises long accepted paths
+        spec, s_spec = run_spec(ps, 80, LLM_CFG, 11)
+    for p, a, b in zip(ps, inc, spec):
+        n0 = len(p) + 1
+        if a.output_tokens != b.output_tokens:
+            # only a numerical tie may separate the two (different KV slot
+            # order -> different fp32 summation order); both must still be
+            # oracle-valid greedy sequences
+            check_tokens_vs_oracle(LLM_CFG, 11, b.output_tokens, n0)
+        else:
+            assert first_divergence(a.output_tokens, b.output_tokens) == len(a.output_tokens)
+    if ssm == "same":
+        assert s_inc.llm_steps >= 1.5 * s_spec.llm_steps  # cpp_inference_tests.sh:191-201

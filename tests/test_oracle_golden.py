@@ -1,0 +1,79 @@
+"""Pin the CPU oracle against HF-transformers golden fixtures (fp32), and
+check its fp16 mode stays within the reference's half-precision tolerance.
+
+HF transformers is the reference's own alignment oracle
+(tests/inference/huggingface_inference.py; per-layer tolerance atol=1e-2 with
+<=5% mismatches in tests/inference/inference_alignment_test.py:193-204).
+"""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+
+TAGS = ["tiny_d64", "tiny_d128"]
+
+
+def test_weight_generator_matches_numpy_twin():
+    from golden.gen_golden import gen_weight
+    for name, kind in [("model.embed_tokens.weight", 0), ("model.norm.weight", 1),
+                       ("model.layers.3.mlp.down_proj.weight", 0)]:
+        a = O.gen_weight(name, 1234, kind, 4099)
+        b = gen_weight(name, 1234, kind, 4099)
+        assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+def test_f16_rounding_matches_numpy():
+    rng = np.random.default_rng(0)
+    x = np.concatenate([rng.standard_normal(20000).astype(np.float32) * s
+                        for s in (1e-7, 1e-5, 1e-3, 1.0, 1e3, 6e4)])
+    x = np.concatenate([x, np.float32([65519.0, 65520.0, 7e4, 0.0, -0.0, 5.96e-8, 2.98e-8])])
+    ours = np.array([O.lib().orc_f2h(float(v)) for v in x], np.uint16)
+    ref = x.astype(np.float16).view(np.uint16)
+    assert np.array_equal(ours, ref)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_fp32_matches_hf_logits_and_hidden(tag):
+    cfg, g = O.load_golden(tag)
+    m = O.Model(cfg, cfg["seed"], fp16=0)
+    prompt = g["prompt"]
+    logits = m.forward(0, prompt, 0)
+    np.testing.assert_allclose(logits, g["logits"], rtol=1e-4, atol=2e-5)
+    L = cfg["num_layers"]
+    for j in range(L):
+        ours = m.hidden(j if j < L - 1 else L, len(prompt))
+        np.testing.assert_allclose(ours, g["hidden"][j], rtol=1e-4, atol=2e-5)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_fp32_greedy_matches_hf(tag):
+    cfg, g = O.load_golden(tag)
+    m = O.Model(cfg, cfg["seed"], fp16=0)
+    toks = m.greedy(0, g["prompt"], cfg["n_new"])
+    assert toks.tolist() == g["greedy"].tolist()
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_fp16_within_half_tolerance(tag):
+    # the reference's half-precision alignment bar: atol 1e-2 w/ <=5% mismatch
+    cfg, g = O.load_golden(tag)
+    m = O.Model(cfg, cfg["seed"], fp16=1)
+    logits = m.forward(0, g["prompt"], 0)
+    bad = np.abs(logits - g["logits"]) > 1e-2
+    assert bad.mean() <= 0.05
+
+
+def test_oracle_batched_decode_matches_per_request():
+    cfg, g = O.load_golden("tiny_d64")
+    m1 = O.Model(cfg, cfg["seed"], fp16=1, max_requests=3, max_seq=64)
+    m2 = O.Model(cfg, cfg["seed"], fp16=1, max_requests=3, max_seq=64)
+    prompts = [[1, 5, 9, 33], [1, 7], [1, 2, 3, 4, 5, 6]]
+    for r, p in enumerate(prompts):
+        m1.forward(r, p, 0)
+        m2.forward(r, p, 0)
+    nxt = [11, 12, 13]
+    pos = [len(p) for p in prompts]
+    lb = m1.decode_batch([0, 1, 2], nxt, pos)
+    for r in range(3):
+        ls = m2.forward(r, [nxt[r]], pos[r])
+        np.testing.assert_array_equal(lb[r], ls[0])

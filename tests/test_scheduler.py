@@ -1,0 +1,132 @@
+"""RequestManager (continuous batching + SpecInfer tree scheduler) on CPU.
+
+Uses the library's hash test double: a model whose next token is a hash of
+exactly the token context its attention would see under the packed KV-slot /
+bitmask rules.  Mirrors the reference's own invariants:
+  * incr decoding == plain greedy decoding of the hash "LM";
+  * SpecInfer tokens == incr-decoding tokens
+    (tests/inference/cpp_inference_tests.sh:183-189);
+  * SpecInfer needs far fewer LLM steps when the SSM agrees
+    (cpp_inference_tests.sh:155-181: incr steps >= 1.5 x spec steps).
+"""
+import numpy as np
+import pytest
+
+import flexflow_amd as fa
+
+M64 = (1 << 64) - 1
+
+
+def mix64(z):
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & M64
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & M64
+    return z ^ (z >> 31)
+
+
+def next_tok(ctx, V):
+    h = 0x243F6A8885A308D3
+    for t in ctx:
+        h = mix64((h + t + 1) & M64)
+    return (h >> 17) % V
+
+
+def expected(prompt, max_length, V, bos=1, eos=()):
+    toks = [bos] + list(prompt)
+    while len(toks) < max_length:
+        toks.append(next_tok(toks, V))
+        if toks[-1] in eos:
+            toks.pop()
+            break
+    return toks
+
+
+def prompts(n, V, lo=3, hi=40, seed=0):
+    rng = np.random.default_rng(seed)
+    return [rng.integers(3, V, size=int(rng.integers(lo, hi))).tolist() for _ in range(n)]
+
+
+V = 997
+
+
+def run_incr(ps, max_length, batch=4, max_tokens=16, eos=()):
+    rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
+                           max_sequence_length=128, eos_token_ids=eos)
+    llm = fa.HashModel(V, "inc", max_requests=batch, max_seq_len=128)
+    res = fa.generate(rm, llm, ps, max_length=max_length)
+    return res, rm.stats()
+
+
+def run_spec(ps, max_length, batch=4, max_tokens=64, widths=(1, 1, 3), disagree=0):
+    rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
+                           max_sequence_length=128, spec_tree_width=widths,
+                           max_spec_tree_token_num=23)
+    llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=128, max_tree_tokens=23)
+    ssm = fa.HashModel(V, "beam", max_requests=batch, max_seq_len=128, max_tree_tokens=23,
+                       salt=1234, disagree_pct=disagree)
+    rm.register_ssm_model(ssm)
+    res = fa.generate(rm, llm, ps, max_length=max_length)
+    return res, rm.stats()
+
+
+@pytest.mark.parametrize("batch,max_tokens", [(1, 8), (4, 16), (8, 128), (3, 5)])
+def test_incr_decoding_matches_greedy(batch, max_tokens):
+    ps = prompts(7, V)
+    res, st = run_incr(ps, 70, batch=batch, max_tokens=max_tokens)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 70, V)
+    assert st.llm_steps > 0
+
+
+def test_incr_decoding_eos_stops_and_is_dropped():
+    ps = prompts(4, V, seed=3)
+    # pick an eos that occurs in one of the greedy continuations
+    full = expected(ps[0], 70, V)
+    eos = full[len(ps[0]) + 5]
+    res, _ = run_incr(ps, 70, eos=(eos,))
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 70, V, eos=(eos,))
+
+
+@pytest.mark.parametrize("disagree", [0, 30, 100])
+@pytest.mark.parametrize("widths", [(1, 1, 3), (), (3,), (1, 2), (2, 1, 1)])
+def test_spec_infer_equals_incr(disagree, widths):
+    ps = prompts(6, V, seed=11)
+    res, st = run_spec(ps, 90, widths=widths, disagree=disagree)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 90, V), (disagree, widths)
+    assert st.llm_steps > 0 and st.ssm_steps == 8 * st.llm_steps or st.ssm_steps > 0
+
+
+def test_spec_infer_prompt_chunking_and_queueing():
+    # more requests than slots, prompts longer than the token budget
+    ps = prompts(9, V, lo=30, hi=60, seed=5)
+    res, _ = run_spec(ps, 100, batch=3, max_tokens=24, disagree=20)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 100, V)
+
+
+def test_spec_infer_step_efficiency():
+    # reference CI bar: incr LLM steps >= 1.5 x spec-infer LLM steps
+    ps = prompts(4, V, seed=7)
+    _, s_inc = run_incr(ps, 100, batch=4, max_tokens=64)
+    res, s_spec = run_spec(ps, 100, batch=4, max_tokens=64, disagree=0)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 100, V)
+    assert s_inc.llm_steps >= 1.5 * s_spec.llm_steps
+    # with a perfect SSM every verify accepts a full 8-deep branch + bonus
+    per_req = [r.llm_decoding_steps for r in res]
+    assert max(per_req) < 20
+
+
+def test_request_limits_rejected():
+    rm = fa.RequestManager(max_sequence_length=32)
+    assert rm.register_new_request(list(range(3, 40)), max_length=10) == 0  # prompt too long
+    assert rm.register_new_request([5, 6], max_length=32) == 0  # max_length >= max_seq
+    assert rm.register_new_request([5, 6], max_length=31) > 0
+
+
+def test_tree_width_limit():
+    with pytest.raises(fa.ffmi.FFMIError):
+        fa.RequestManager(spec_tree_width=(4,))  # MAX_BEAM_WIDTH = 3 (request_manager.cc:168)
+    with pytest.raises(fa.ffmi.FFMIError):
+        fa.RequestManager(spec_tree_width=(2, 2))  # 4 nodes/layer > 3 (request_manager.cc:1685)
