@@ -252,14 +252,48 @@ extern "C" ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, 
   return FFMI_OK;
 }
 
+extern "C" size_t ffmi_linear_workspace_bytes(int T, int out_dim, int in_dim, int epilogue) {
+  if (T <= 0 || out_dim <= 0 || in_dim <= 0) return 0;
+  return ffmi::gemm_workspace_bytes(T, out_dim, in_dim, epilogue);
+}
+
+extern "C" ffmi_status ffmi_linear_ws(const void *X, const void *W_packed, void *Y, int T,
+                                      int out_dim, int in_dim, int epilogue, void *workspace,
+                                      size_t workspace_bytes, ffmi_stream stream) {
+  FFMI_CHECK(X && W_packed && Y && T >= 0 && out_dim > 0, FFMI_ERR_INVALID);
+  FFMI_CHECK(in_dim > 0 && in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
+  FFMI_CHECK(epilogue == FFMI_EPI_NONE || epilogue == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_gemm((const uint16_t *)X, (const uint16_t *)W_packed, (uint16_t *)Y,
+                             (float *)workspace, workspace_bytes, T, out_dim, in_dim, epilogue,
+                             (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+static std::mutex g_ws_mu;
+static void *g_ws = nullptr;
+static size_t g_ws_bytes = 0;
+
 extern "C" ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
                                    int out_dim, int in_dim, int epilogue, ffmi_stream stream) {
   FFMI_CHECK(X && W_packed && Y && T >= 0 && out_dim > 0, FFMI_ERR_INVALID);
   FFMI_CHECK(in_dim > 0 && in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
-  FFMI_CHECK(epilogue == FFMI_EPI_NONE || epilogue == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
-  FFMI_HIP(ffmi::launch_gemm((const uint16_t *)X, (const uint16_t *)W_packed, (uint16_t *)Y, T,
-                             out_dim, in_dim, epilogue, (hipStream_t)stream));
-  return FFMI_OK;
+  const size_t need = ffmi_linear_workspace_bytes(T, out_dim, in_dim, epilogue);
+  void *ws = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if (need > g_ws_bytes) {
+      if (g_ws) {
+        FFMI_HIP(hipDeviceSynchronize());
+        (void)hipFree(g_ws);
+        g_ws = nullptr;
+        g_ws_bytes = 0;
+      }
+      if (hipMalloc(&g_ws, need) != hipSuccess) return FFMI_ERR_OOM;
+      g_ws_bytes = need;
+    }
+    ws = g_ws;
+  }
+  return ffmi_linear_ws(X, W_packed, Y, T, out_dim, in_dim, epilogue, ws, g_ws_bytes, stream);
 }
 
 extern "C" ffmi_status ffmi_rmsnorm(const void *x, const void *w, void *out, int T, int H,

@@ -61,8 +61,9 @@ hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
 hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
                               int N, int K, uint16_t *dst, int interleave_gate_up,
                               int tile_offset, hipStream_t s);
-hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T,
-                       int N, int K, int epilogue, hipStream_t s);
+hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
+                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s);
+size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
                           hipStream_t s);

@@ -24,6 +24,16 @@
 
 namespace ffmi {
 
+// SigmoidSiluMultiKernel numerics (sigmoid_silu_multi.cu:41-46): gate and up
+// are fp16 values, out = half(half(g * half(sigmoid(g))) * u)
+__device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
+  const float g = __half2float(__float2half_rn(gacc));
+  const float u = __half2float(__float2half_rn(uacc));
+  const float sg = __half2float(__float2half_rn(1.0f / (1.0f + expf(-g))));
+  const float t = __half2float(__float2half_rn(g * sg));
+  return __half_as_ushort(__float2half_rn(t * u));
+}
+
 // MULTI = 1 marks the multi-pass (T > 192, prefill) instantiation so that
 // profiles separate it from the single-pass decode/verify launches.
 template <int MT, int NT, int KW, int U, int EPI, int MULTI>
@@ -144,12 +154,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         for (int r = 0; r < 4; ++r) {
           int m = m0 + i * 16 + (lane >> 4) * 4 + r;
           if (m >= T) continue;
-          float g = __half2float(__float2half_rn(acc[i][0][r]));
-          float u = __half2float(__float2half_rn(acc[i][1][r]));
-          float sg = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-g)));
-          float sh = __half2float(__float2half_rn(sg));
-          float t = __half2float(__float2half_rn(__fmul_rn(g, sh)));
-          Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(__fmul_rn(t, u)));
+          Y[(size_t)m * N + n] = silu_mul_h(acc[i][0][r], acc[i][1][r]);
         }
     }
   }
@@ -179,11 +184,218 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
   return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s);
 }
 
-hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T, int N,
-                       int K, int epilogue, hipStream_t s) {
+// ---------------------------------------------------------------------------
+// M-split GEMM for 64 < T (verify batches, SSM init, prefill blocks).
+//
+// The skinny kernel above re-reads the whole activation block from L2 in
+// every wave (K split over waves) and runs at 1 wave/SIMD at T ~ 168, which
+// made it latency-bound (~0.7 TB/s).  Here the 4 waves of a workgroup split
+// the ROWS (MTW m-tiles each, 64*MTW rows per block) and share one weight
+// tile of NTW 16-column tiles per 32-deep k-step, staged through LDS with a
+// register double buffer (load k+1 while the MFMAs of k run, one barrier per
+// k-step).  Each wave loads only its own rows of X.  Small-N layers are
+// split over K across workgroups (S slices, fp32 partials reduced in slice
+// order by gemm_reduce_kernel), so every layer puts >= ~256 workgroups on
+// the 256 CUs.  Reduction order per output element: MFMA chain over the
+// slice's k-steps, then slices 0..S-1 -- fixed by (N, K, S), not by T.
+// ---------------------------------------------------------------------------
+template <int MTW, int NTW, int EPI>
+__global__ __launch_bounds__(256) void gemm_mid_kernel(
+    const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
+    uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
+    int NTILES, int S) {
+  static_assert(NTW % 4 == 0, "NTW pieces are spread over 4 waves");
+  constexpr int PPT = NTW / 4;
+  __shared__ __attribute__((aligned(16))) h8 sB[2][NTW][64];
+  const int lane = threadIdx.x & 63;
+  const int wave = threadIdx.x >> 6;
+  const int tile0 = blockIdx.x * NTW;
+  const int ks = blockIdx.y;
+  const int m0 = blockIdx.z * (4 * MTW * 16) + wave * MTW * 16;
+  const int per = (KT + S - 1) / S;
+  const int kb = min(KT, ks * per);
+  const int ke = min(KT, kb + per);
+
+  const uint16_t *bsrc[PPT];
+  int bj[PPT];
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    bj[p] = wave + 4 * p;
+    const int t = min(tile0 + bj[p], NTILES - 1);
+    bsrc[p] = Wp + (size_t)t * KT * 512 + lane * 8;
+  }
+  const uint16_t *xrow[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    const int r = min(m0 + i * 16 + (lane & 15), T - 1);
+    xrow[i] = X + (size_t)r * K + 8 * (lane >> 4);
+  }
+  f4 acc[MTW][NTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+  if (kb < ke) {
+    h8 bst[PPT], a[MTW];
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) bst[p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kb * 512);
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) a[i] = *reinterpret_cast<const h8 *>(xrow[i] + kb * 32);
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) sB[0][bj[p]][lane] = bst[p];
+    __syncthreads();
+    int cur = 0;
+    for (int kt = kb; kt < ke; ++kt) {
+      const int kn = min(kt + 1, ke - 1);  // clamped prefetch: branch-free
+      h8 an[MTW];
+#pragma unroll
+      for (int p = 0; p < PPT; ++p)
+        bst[p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kn * 512);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) an[i] = *reinterpret_cast<const h8 *>(xrow[i] + kn * 32);
+      h8 b[NTW];
+#pragma unroll
+      for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int j = 0; j < NTW; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bst[p];
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) a[i] = an[i];
+      cur ^= 1;
+    }
+  }
+
+  // C/D layout: col = lane&15, row = (lane>>4)*4 + r
+  if (S > 1) {
+    const int NP = NTILES * 16;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int tile = tile0 + j;
+      if (tile >= NTILES) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Ypart[((size_t)ks * T + m) * NP + tile * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  if (EPI == 0) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (tile0 + j) * 16 + (lane & 15);
+      if (tile0 + j >= NTILES || n >= N) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
+        }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NTW; j += 2) {
+      const int n = ((tile0 + j) >> 1) * 16 + (lane & 15);
+      if (tile0 + j >= NTILES || n >= N) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Y[(size_t)m * N + n] = silu_mul_h(acc[i][j][r], acc[i][j + 1][r]);
+        }
+    }
+  }
+}
+
+// Sum the S fp32 partial slabs in slice order, then the epilogue.
+template <int EPI>
+__global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__restrict__ Y,
+                                   int T, int N, int NTILES, int S) {
+  const int NP = NTILES * 16;
+  const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
+  if (idx >= (long)T * N) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
+  if (EPI == 0) {
+    float acc = Ypart[(size_t)m * NP + n];
+    for (int s = 1; s < S; ++s) acc += Ypart[((size_t)s * T + m) * NP + n];
+    Y[idx] = __half_as_ushort(__float2half_rn(acc));
+  } else {
+    const int gcol = (n >> 4) * 32 + (n & 15);
+    float g = Ypart[(size_t)m * NP + gcol], u = Ypart[(size_t)m * NP + gcol + 16];
+    for (int s = 1; s < S; ++s) {
+      g += Ypart[((size_t)s * T + m) * NP + gcol];
+      u += Ypart[((size_t)s * T + m) * NP + gcol + 16];
+    }
+    Y[idx] = silu_mul_h(g, u);
+  }
+}
+
+static int mid_split(int KT, int blocks) {
+  int S = (256 + blocks - 1) / blocks;
+  S = S < 1 ? 1 : (S > 8 ? 8 : S);
+  return S > KT ? KT : S;
+}
+
+size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
+  const int mtiles = (T + 15) / 16;
+  if (mtiles <= 4) return 0;
+  const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
+  const int MTW = mtiles <= 8 ? 2 : 3;
+  const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
+  const int nblk = (ntiles + 7) / 8;
+  const int S = mid_split(K / 32, nblk * mblocks);
+  return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
+}
+
+template <int MTW>
+static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
+                          size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s) {
+  constexpr int NTW = 8;
+  const int KT = K / 32;
+  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
+  const int mtiles = (T + 15) / 16;
+  const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
+  const int nblk = (ntiles + NTW - 1) / NTW;
+  int S = mid_split(KT, nblk * mblocks);
+  const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
+  if (S > 1 && (!ws || ws_bytes < need)) S = 1;  // no workspace: un-split (slower)
+  dim3 grid(nblk, S, mblocks);
+  if (epi)
+    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
+                       K, KT, ntiles, S);
+  else
+    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
+                       K, KT, ntiles, S);
+  if (S > 1) {
+    const long total = (long)T * N;
+    const unsigned blocks = (unsigned)((total + 255) / 256);
+    if (epi)
+      hipLaunchKernelGGL(gemm_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
+                         ntiles, S);
+    else
+      hipLaunchKernelGGL(gemm_reduce_kernel<0>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
+                         ntiles, S);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
+                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s) {
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
   const int mtiles = (T + 15) / 16;
+  if (mtiles > 8) return run_mid<3>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
+  if (mtiles > 4) return run_mid<2>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
   if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
   if (mtiles <= 2) return dispatch_nt<2, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
   if (mtiles <= 4) return dispatch_nt<4, 4, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);

@@ -43,6 +43,8 @@ struct LlamaGPU : public ffmi_model {
            *mlp = nullptr, *logits = nullptr;
   int32_t *ids_d = nullptr;
   float *probs_d = nullptr;
+  float *ws = nullptr;  // split-K workspace of the GEMMs
+  size_t ws_bytes = 0;
   int32_t *ids_h = nullptr;
   float *probs_h = nullptr;
   ffmi_batch_dev *batch = nullptr;
@@ -190,6 +192,15 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&mlp, (size_t)Tm * Fl));
     TRY(alloc(&logits, (size_t)Tm * V));
     TRY(alloc(&ids_d, (size_t)Tm * 4));
+    {
+      const size_t w1 = ffmi_linear_workspace_bytes(Tm, 3 * Hl, H, FFMI_EPI_NONE);
+      const size_t w2 = ffmi_linear_workspace_bytes(Tm, H, Hl, FFMI_EPI_NONE);
+      const size_t w3 = ffmi_linear_workspace_bytes(Tm, Fl, H, FFMI_EPI_SILU_MUL);
+      const size_t w4 = ffmi_linear_workspace_bytes(Tm, H, Fl, FFMI_EPI_NONE);
+      const size_t w5 = ffmi_linear_workspace_bytes(Tm, V, H, FFMI_EPI_NONE);
+      ws_bytes = std::max(std::max(std::max(w1, w2), std::max(w3, w4)), w5);
+      if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
+    }
     TRY(alloc(&probs_d, (size_t)Tm * 4));
     FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * sizeof(int32_t), 0));
     FFMI_HIP(hipHostMalloc((void **)&probs_h, (size_t)Tm * 4 * sizeof(float), 0));
@@ -301,7 +312,7 @@ struct LlamaGPU : public ffmi_model {
         TRY(ffmi_residual_rmsnorm(res, proj, L.in_norm, res, h, T, H, eps, s));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 2 : 4), 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE, s));
+      TRY(ffmi_linear_ws(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE, ws, ws_bytes, s));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
       pr = prof_begin(on);
       if (mode == FFMI_MODEL_TREE)
@@ -312,7 +323,7 @@ struct LlamaGPU : public ffmi_model {
         TRY(ffmi_attn_inc(L.attn, batch, qkv, att, s));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE, s));
+      TRY(ffmi_linear_ws(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE, ws, ws_bytes, s));
       prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
@@ -321,10 +332,10 @@ struct LlamaGPU : public ffmi_model {
       TRY(ffmi_residual_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, s));
       prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL, s));
+      TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       pr = prof_begin(on);
-      TRY(ffmi_linear(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE, s));
+      TRY(ffmi_linear_ws(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE, ws, ws_bytes, s));
       prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
@@ -334,7 +345,7 @@ struct LlamaGPU : public ffmi_model {
     TRY(ffmi_residual_rmsnorm(res, proj, final_norm, res, h, T, H, eps, s));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
     pr = prof_begin(ptail);
-    TRY(ffmi_linear(h, lm, logits, T, V, H, FFMI_EPI_NONE, s));
+    TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
     pr = prof_begin(ptail);
     if (k == 1)

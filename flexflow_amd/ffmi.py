@@ -111,6 +111,9 @@ SIGNATURES = {
     "ffmi_linear_pack_weight": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_linear_pack_gate_up": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_linear": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "ffmi_linear_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
+    "ffmi_linear_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                               c_size_t, c_void_p]),
     "ffmi_rmsnorm": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "ffmi_residual_rmsnorm": (c_int, [c_void_p] * 5 + [c_int, c_int, c_float, c_void_p]),
     "ffmi_comm_unique_id": (c_int, [c_void_p]),

@@ -154,9 +154,16 @@ ffmi_status ffmi_linear_pack_weight(const void *W, int out_dim, int in_dim,
                                     void *W_packed, ffmi_stream stream);
 ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, int out_dim,
                                      int in_dim, void *W_packed, ffmi_stream stream);
-/* Y[T][out] = X[T][in] . W^T, fp16 in/out, fp32 accumulate. */
+/* Y[T][out] = X[T][in] . W^T, fp16 in/out, fp32 accumulate.  Uses a
+ * library-owned split-K workspace: calls on different streams must not
+ * overlap (use ffmi_linear_ws for that). */
 ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
                         int out_dim, int in_dim, int epilogue, ffmi_stream stream);
+/* same with a caller-owned workspace of ffmi_linear_workspace_bytes() bytes */
+size_t ffmi_linear_workspace_bytes(int T, int out_dim, int in_dim, int epilogue);
+ffmi_status ffmi_linear_ws(const void *X, const void *W_packed, void *Y, int T,
+                           int out_dim, int in_dim, int epilogue, void *workspace,
+                           size_t workspace_bytes, ffmi_stream stream);
 
 /* ------------------------------------------------------------------------ */
 /* Norms (replace Kernels::RMSNorm / ResidualRMSNorm inference_kernel_wrapper, */

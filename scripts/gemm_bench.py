@@ -1,0 +1,69 @@
+"""GEMM / kernel microbenchmark through the C ABI (HIP events, one process).
+
+    python scripts/gemm_bench.py [--shapes llama7b|ssm] [--T 1,8,168]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import flexflow_amd.ffmi as F  # noqa: E402
+from hip_util import Buf, Timer, f16, hip  # noqa: E402
+
+SHAPES = {
+    "llama7b": [("qkv", 12288, 4096, 0), ("o", 4096, 4096, 0), ("gate_up", 11008, 4096, 1),
+                ("down", 4096, 11008, 0), ("lm_head", 32000, 4096, 0)],
+    "ssm": [("qkv", 2304, 768, 0), ("o", 768, 768, 0), ("gate_up", 3072, 768, 1),
+            ("down", 768, 3072, 0), ("lm_head", 32000, 768, 0)],
+}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--shapes", default="llama7b")
+    ap.add_argument("--T", default="1,8,24,64,168,192")
+    ap.add_argument("--iters", type=int, default=20)
+    args = ap.parse_args()
+    L = F.lib()
+    rng = np.random.default_rng(0)
+    res = []
+    for name, N, K, epi in SHAPES[args.shapes]:
+        rows = 2 * N if epi else N
+        W = f16(rng.uniform(-0.05, 0.05, (rows, K)))
+        nb = L.ffmi_linear_packed_bytes(rows, K)
+        src = Buf(W)
+        Wp = Buf.empty((nb // 2,), np.uint16)
+        if epi:
+            half = rows // 2
+            g, u = Buf(W[:half]), Buf(W[half:])
+            F.check(L.ffmi_linear_pack_gate_up(g.ptr, u.ptr, half, K, Wp.ptr, None))
+        else:
+            F.check(L.ffmi_linear_pack_weight(src.ptr, N, K, Wp.ptr, None))
+        del src
+        for T in [int(t) for t in args.T.split(",")]:
+            X = Buf(f16(rng.standard_normal((T, K))))
+            Y = Buf.empty((T, N), np.float16)
+            for _ in range(3):
+                F.check(L.ffmi_linear(X.ptr, Wp.ptr, Y.ptr, T, N, K, epi, None))
+            tm = Timer()
+            tm.start()
+            for _ in range(args.iters):
+                L.ffmi_linear(X.ptr, Wp.ptr, Y.ptr, T, N, K, epi, None)
+            ms = tm.stop() / args.iters
+            byts = 2.0 * (rows * K + T * K + T * N)
+            r = dict(op=name, T=T, N=N, K=K, us=round(ms * 1e3, 2),
+                     GBps=round(byts / (ms * 1e-3) / 1e9, 1),
+                     TFLOPs=round(2.0 * T * rows * K / (ms * 1e-3) / 1e12, 1))
+            res.append(r)
+            print(json.dumps(r), flush=True)
+    return res
+
+
+if __name__ == "__main__":
+    main()

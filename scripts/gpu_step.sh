@@ -1,0 +1,12 @@
+#!/bin/bash
+# Run one GPU step under its own time limit; stop the chain on anything that
+# is not a clean pass/fail (faults, aborts, timeouts).
+#   scripts/gpu_step.sh NAME SECONDS cmd...
+name=$1; secs=$2; shift 2
+mkdir -p gpurun_out
+timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+rc=$?
+echo "[$name] rc=$rc"
+tail -n 25 "gpurun_out/$name.log"
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit 99; fi
+exit 0
