@@ -91,7 +91,22 @@ extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_des
   h.num_commits = d->num_commits;
   h.num_mask_reqs = d->num_mask_reqs;
   h.off_tokens = (int)off;
-  memcpy(b->host + off, d->tokens, d->num_tokens * sizeof(ffmi_token_info));
+  {
+    // kernels read the query-major visibility word; derive it here from the
+    // reference's key-major per-request bitmask (the caller's value is ignored)
+    ffmi_token_info *tk = reinterpret_cast<ffmi_token_info *>(b->host + off);
+    memcpy(tk, d->tokens, d->num_tokens * sizeof(ffmi_token_info));
+    for (int t = 0; t < d->num_tokens; ++t) {
+      uint64_t v = 0;
+      const int r = tk[t].req, n = tk[t].tree_len < FFMI_MAX_TREE ? tk[t].tree_len : FFMI_MAX_TREE;
+      const int bit = tk[t].tree_bit;
+      if (n > 0 && r >= 0 && r < d->num_mask_reqs && bit >= 0 && bit < 64) {
+        const uint64_t *m = d->masks + (size_t)r * FFMI_MAX_TREE;
+        for (int j = 0; j < n; ++j) v |= ((m[j] >> bit) & 1ull) << j;
+      }
+      tk[t].tree_vis = v;
+    }
+  }
   off += align16(d->num_tokens * sizeof(ffmi_token_info));
   h.off_work = (int)off;
   memcpy(b->host + off, d->work, d->num_work * sizeof(ffmi_attn_work));
@@ -99,10 +114,9 @@ extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_des
   h.off_commits = (int)off;
   if (d->num_commits) memcpy(b->host + off, d->commits, d->num_commits * sizeof(ffmi_commit_info));
   off += align16(d->num_commits * sizeof(ffmi_commit_info));
+  // the bitmask table itself stays on the host (folded into tree_vis above)
+  h.num_mask_reqs = 0;
   h.off_masks = (int)off;
-  if (d->num_mask_reqs)
-    memcpy(b->host + off, d->masks, (size_t)d->num_mask_reqs * FFMI_MAX_TREE * sizeof(uint64_t));
-  off += (size_t)d->num_mask_reqs * FFMI_MAX_TREE * sizeof(uint64_t);
   memcpy(b->host, &h, sizeof(h));
   FFMI_CHECK(off <= b->cap, FFMI_ERR_INVALID);
   FFMI_HIP(hipMemcpyAsync(b->dev, b->host, off, hipMemcpyHostToDevice, (hipStream_t)stream));

@@ -130,12 +130,12 @@ hipError_t launch_commit(const char *blob, int C, const uint16_t *stage, uint16_
   return hipGetLastError();
 }
 
-__device__ __forceinline__ bool key_visible(int slot, const ffmi_token_info &ti,
-                                            const uint64_t *mask) {
-  if (slot < ti.prefix_len) return true;
-  const unsigned j = (unsigned)(slot - ti.tree_base);
-  if (j < (unsigned)ti.tree_len) return (mask[j] >> ti.tree_bit) & 1ull;
-  return false;
+// visibility from registers only: prefix range + the query's 64-bit tree word
+__device__ __forceinline__ bool key_visible(int slot, int prefix_len, int tree_base,
+                                            int tree_len, uint64_t tree_vis) {
+  if (slot < prefix_len) return true;
+  const unsigned j = (unsigned)(slot - tree_base);
+  return j < (unsigned)tree_len && ((tree_vis >> j) & 1ull);
 }
 
 template <int D>
@@ -159,7 +159,8 @@ __global__ __launch_bounds__(256) void attention_kernel(
   const int Hl = heads * D;
   const bool qvalid = qi < w.q_count;
   const ffmi_token_info ti = bv.tokens[w.q_start + (qvalid ? qi : 0)];
-  const uint64_t *mask = bv.masks + (size_t)w.req * FFMI_MAX_TREE;
+  const int pre = ti.prefix_len, tb = ti.tree_base, tl = ti.tree_len;
+  const uint64_t tv = ti.tree_vis;
 
   h8 qf[KS];
 #pragma unroll
@@ -208,7 +209,7 @@ __global__ __launch_bounds__(256) void attention_kernel(
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int slot = base + (j >> 2) * 16 + 4 * g + (j & 3);
-      vis[j] = qvalid && slot < w.kv_len && key_visible(slot, ti, mask);
+      vis[j] = qvalid && slot < w.kv_len && key_visible(slot, pre, tb, tl, tv);
       sc[j] = __fmul_rn(scale, s[j >> 2][j & 3]);
       cmax = vis[j] ? fmaxf(cmax, sc[j]) : cmax;
     }

@@ -236,38 +236,56 @@ __global__ __launch_bounds__(256) void gemm_mid_kernel(
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // Software pipeline (per k-step: one barrier, weight tile double-buffered
+  // in LDS).  Weight loads run PF=3 k-steps ahead in a register ring, X
+  // fragments one step ahead; X(k+1) is issued BEFORE B(k+3) so that the
+  // in-order vmcnt wait for X(k+1) never forces the younger weight loads.
   if (kb < ke) {
-    h8 bst[PPT], a[MTW];
+    constexpr int PF = 3;
+    h8 bq[PF][PPT];
+    h8 a[MTW], an[MTW];
 #pragma unroll
-    for (int p = 0; p < PPT; ++p) bst[p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kb * 512);
+    for (int q = 0; q < PF; ++q) {
+      const int kq = min(kb + q, ke - 1);
+#pragma unroll
+      for (int p = 0; p < PPT; ++p)
+        bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
+    }
 #pragma unroll
     for (int i = 0; i < MTW; ++i) a[i] = *reinterpret_cast<const h8 *>(xrow[i] + kb * 32);
 #pragma unroll
-    for (int p = 0; p < PPT; ++p) sB[0][bj[p]][lane] = bst[p];
+    for (int p = 0; p < PPT; ++p) sB[0][bj[p]][lane] = bq[0][p];
     __syncthreads();
     int cur = 0;
-    for (int kt = kb; kt < ke; ++kt) {
-      const int kn = min(kt + 1, ke - 1);  // clamped prefetch: branch-free
-      h8 an[MTW];
+    for (int kt0 = kb; kt0 < ke; kt0 += PF) {
 #pragma unroll
-      for (int p = 0; p < PPT; ++p)
-        bst[p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kn * 512);
+      for (int q = 0; q < PF; ++q) {
+        const int kt = kt0 + q;
+        if (kt >= ke) break;
+        const int kx = min(kt + 1, ke - 1);
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) an[i] = *reinterpret_cast<const h8 *>(xrow[i] + kn * 32);
-      h8 b[NTW];
+        for (int i = 0; i < MTW; ++i) an[i] = *reinterpret_cast<const h8 *>(xrow[i] + kx * 32);
+        // slot q held B(kt); it is free once B(kt) went to LDS (previous step)
+        const int kw = min(kt + PF, ke - 1);
+        h8 b[NTW];
 #pragma unroll
-      for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
+        for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+        for (int p = 0; p < PPT; ++p)
+          bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
 #pragma unroll
-        for (int j = 0; j < NTW; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int i = 0; i < MTW; ++i)
 #pragma unroll
-      for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bst[p];
-      __syncthreads();
+          for (int j = 0; j < NTW; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+        // B(kt+1) lives in ring slot (q+1) % PF
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) a[i] = an[i];
-      cur ^= 1;
+        for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bq[(q + 1) % PF][p];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < MTW; ++i) a[i] = an[i];
+        cur ^= 1;
+      }
     }
   }
 

@@ -202,11 +202,112 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
   }
 }
 
+// Register-resident variant: one 512-thread workgroup per row reads the row
+// ONCE as 16-B vectors (NV per thread) and does max, sum and the k selection
+// rounds from registers.  Same arithmetic and tie rule as the kernel above.
+template <int NV>
+__global__ __launch_bounds__(512) void softmax_topk_reg_kernel(
+    const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
+    float *__restrict__ probs) {
+  __shared__ float fscratch[8];
+  __shared__ unsigned long long kscratch[8];
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int nvec = V >> 3;
+  const uint4 *x = reinterpret_cast<const uint4 *>(logits + (size_t)row * V);
+  uint4 r[NV];
+#pragma unroll
+  for (int v = 0; v < NV; ++v) {
+    const int i = v * 512 + tid;
+    r[v] = i < nvec ? x[i] : make_uint4(0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u);
+  }
+  auto elem = [&](int v, int e) -> float {
+    const uint32_t w = (&r[v].x)[e >> 1];
+    return h2f_((uint16_t)((e & 1) ? (w >> 16) : (w & 0xffffu)));
+  };
+  float mx = -INFINITY;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) mx = fmaxf(mx, elem(v, e));
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  if (lane == 0) fscratch[wv] = mx;
+  __syncthreads();
+  mx = fscratch[0];
+#pragma unroll
+  for (int q = 1; q < 8; ++q) mx = fmaxf(mx, fscratch[q]);
+  __syncthreads();
+  float se = 0.f;
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+    if (v * 512 + tid < nvec)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) se += expf(elem(v, e) - mx);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+  if (lane == 0) fscratch[wv] = se;
+  __syncthreads();
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) sum += fscratch[q];
+  int chosen[4] = {-1, -1, -1, -1};
+  for (int rd = 0; rd < k; ++rd) {
+    unsigned long long best = 0;
+#pragma unroll
+    for (int v = 0; v < NV; ++v) {
+      const int base = (v * 512 + tid) * 8;
+      if (base >= V) continue;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int i = base + e;
+        bool taken = false;
+        for (int q = 0; q < rd; ++q) taken |= (chosen[q] == i);
+        if (taken) continue;
+        const uint16_t p = f2h_(__fdiv_rn(expf(elem(v, e) - mx), sum));
+        const unsigned long long key =
+            ((unsigned long long)p << 32) | (unsigned long long)(0xffffffffu - (unsigned)i);
+        best = key > best ? key : best;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      unsigned long long other = __shfl_xor(best, o);
+      best = other > best ? other : best;
+    }
+    __syncthreads();
+    if (lane == 0) kscratch[wv] = best;
+    __syncthreads();
+    unsigned long long b = kscratch[0];
+#pragma unroll
+    for (int q = 1; q < 8; ++q) b = kscratch[q] > b ? kscratch[q] : b;
+    const int idx = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    chosen[rd] = idx;
+    if (tid == 0) {
+      ids[(size_t)row * k + rd] = idx;
+      if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)(b >> 32));
+    }
+  }
+}
+
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
                          float *probs, hipStream_t s) {
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
+  const int nv = (V / 8 + 511) / 512;
+  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 16) {
+    if (nv <= 1)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+    else if (nv <= 2)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+    else if (nv <= 4)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+    else if (nv <= 8)
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<8>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+    else
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<16>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+  } else {
+    hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
+  }
   return hipGetLastError();
 }
 

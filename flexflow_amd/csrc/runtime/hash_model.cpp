@@ -48,14 +48,12 @@ struct HashModel : public ffmi_model {
     hs->resize(ps.tokens.size());
     for (size_t t = 0; t < ps.tokens.size(); ++t) {
       const auto &ti = ps.tokens[t];
-      const uint64_t *mask =
-          ps.num_mask_reqs ? &ps.masks[(size_t)ti.req * FFMI_MAX_TREE] : nullptr;
       const int end = std::max(ti.prefix_len, ti.tree_base + ti.tree_len);
       uint64_t h = 0x243F6A8885A308D3ull;
       for (int s = 0; s < end; ++s) {
         bool vis = s < ti.prefix_len;
-        if (!vis && s >= ti.tree_base && s < ti.tree_base + ti.tree_len && mask)
-          vis = (mask[s - ti.tree_base] >> ti.tree_bit) & 1ull;
+        if (!vis && s >= ti.tree_base && s < ti.tree_base + ti.tree_len)
+          vis = (ti.tree_vis >> (s - ti.tree_base)) & 1ull;
         if (!vis) continue;
         h = mix64(h + (uint64_t)(int64_t)cache[slot_of(ti.req, s)] + 1);
       }

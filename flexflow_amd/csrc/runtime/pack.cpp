@@ -42,6 +42,17 @@ static void build_work(PackedStep *ps) {
   }
 }
 
+// transpose the request's key-major bitmask into the query's visibility word
+static void fill_tree_vis(PackedStep *ps) {
+  for (auto &ti : ps->tokens) {
+    ti.tree_vis = 0;
+    if (ti.tree_len <= 0 || ps->num_mask_reqs == 0) continue;
+    const uint64_t *m = &ps->masks[(size_t)ti.req * FFMI_MAX_TREE];
+    const int n = std::min(ti.tree_len, FFMI_MAX_TREE);
+    for (int j = 0; j < n; ++j) ti.tree_vis |= ((m[j] >> ti.tree_bit) & 1ull) << j;
+  }
+}
+
 static void clamp_slots(PackedStep *ps, int slots) {
   for (auto &ti : ps->tokens) {
     if (ti.store_slot >= slots) ti.store_slot = -1;
@@ -77,6 +88,7 @@ void pack_inc(const BatchConfig &bc, int max_requests, int slots, PackedStep *ps
     ti.tree_base = 0;
     ti.tree_len = 0;
     ti.tree_bit = 0;
+    ti.tree_vis = 0;
   }
   (void)max_requests;
   clamp_slots(ps, slots);
@@ -117,6 +129,7 @@ void pack_tree(const TreeVerifyBatchConfig &bc, int max_requests, int slots, Pac
     }
   }
   clamp_slots(ps, slots);
+  fill_tree_vis(ps);
   build_work(ps);
 }
 
@@ -159,6 +172,7 @@ void pack_beam(const BeamSearchBatchConfig &bc, int max_requests, int slots,
     }
   }
   clamp_slots(ps, slots);
+  fill_tree_vis(ps);
   build_work(ps);
 }
 

@@ -260,6 +260,7 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
       std::vector<TokenDepth> verified_tokens =
           traverse_verify_tree(guid, dfs_tree_inputs.at(guid), tree_outputs);
       stats.tokens_committed += (long)verified_tokens.size();
+      stats.request_verifies++;
       if ((int)(verified_tokens.size() + request.tokens.size()) >= request.max_length) {
         for (const auto &tp : verified_tokens)
           if (tp.second < request.max_length) request.tokens.push_back(tp.first);

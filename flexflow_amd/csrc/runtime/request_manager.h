@@ -126,6 +126,7 @@ class RequestManager {
   const ProfileInfo *get_profile(RequestGuid guid) const;
   struct Stats {
     long llm_steps = 0, ssm_steps = 0, tokens_committed = 0, tree_tokens_verified = 0;
+    long request_verifies = 0;
     double wall_us = 0;
   } stats;
 

@@ -27,7 +27,7 @@ MAX_TREE = 64
 class TokenInfo(ctypes.Structure):
     _fields_ = [(n, ctypes.c_int32) for n in
                 ("token_id", "pos", "req", "store_slot", "prefix_len", "tree_base",
-                 "tree_len", "tree_bit")]
+                 "tree_len", "tree_bit")] + [("tree_vis", ctypes.c_uint64)]
 
 
 class AttnWork(ctypes.Structure):
@@ -92,7 +92,8 @@ class OpStat(ctypes.Structure):
 
 class ServeStats(ctypes.Structure):
     _fields_ = [("llm_steps", c_long), ("ssm_steps", c_long), ("tokens_committed", c_long),
-                ("tree_tokens_verified", c_long), ("wall_us", c_double)]
+                ("tree_tokens_verified", c_long), ("request_verifies", c_long),
+                ("wall_us", c_double)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ffmi.h

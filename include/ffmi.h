@@ -62,6 +62,9 @@ typedef struct {
   int32_t tree_base;  /* first tree slot                                     */
   int32_t tree_len;   /* tree slots [tree_base, tree_base+tree_len) ...      */
   int32_t tree_bit;   /* ... visible iff mask[req][slot-tree_base] bit set   */
+  uint64_t tree_vis;  /* OUTPUT of ffmi_batch_upload (input ignored): the same
+                         rule transposed for this query, bit j set iff tree
+                         slot tree_base+j is visible -- what kernels read */
 } ffmi_token_info;
 
 typedef struct {
@@ -290,6 +293,7 @@ ffmi_status ffmi_rm_get_profile(ffmi_rm *rm, int64_t guid, ffmi_profile *p);
 /* aggregate counters of the last serve call */
 typedef struct {
   long llm_steps, ssm_steps, tokens_committed, tree_tokens_verified;
+  long request_verifies; /* (request, verify step) pairs that committed tokens */
   double wall_us;
 } ffmi_serve_stats;
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
