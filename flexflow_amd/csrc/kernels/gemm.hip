@@ -20,6 +20,11 @@
 //    row's result does not depend on T or on which other rows are batched.
 // Epilogue FFMI_EPI_SILU_MUL fuses SigmoidSiluMulti (sigmoid_silu_multi.cu:
 // 37-47) on interleaved [gate|up] tiles.
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+
 #include "../ffmi_internal.h"
 
 namespace ffmi {
@@ -34,17 +39,29 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
   return __half_as_ushort(__float2half_rn(t * u));
 }
 
-// MULTI = 1 marks the multi-pass (T > 192, prefill) instantiation so that
-// profiles separate it from the single-pass decode/verify launches.
+// MULTI = 1: multi-pass over row blocks of MT*16 rows.  The grid is 1-D and
+// XCD-grouped: the row blocks of one column block get linear ids 8 apart
+// (ids are dealt round-robin over the 8 XCDs), so they run together on ONE
+// XCD and the weight tile crosses HBM once and is re-read from that XCD's
+// L2 by the sibling row blocks (MI355X_MICROARCH.md ring-vs-splitk: "tiles
+// with the rows split").
 template <int MT, int NT, int KW, int U, int EPI, int MULTI>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *__restrict__ Y, int T, int N, int K, int KT, int NTILES) {
+    uint16_t *__restrict__ Y, int T, int N, int K, int KT, int NTILES, int mpasses) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  const int tile0 = blockIdx.x * NT;
-  const int m0 = blockIdx.y * (MT * 16);
+  int cb = blockIdx.x, mb = 0;
+  if (MULTI) {
+    const int grp = 8 * mpasses;
+    const int r = blockIdx.x % grp;
+    cb = (blockIdx.x / grp) * 8 + (r & 7);
+    mb = r >> 3;
+    if (cb * NT >= NTILES) return;
+  }
+  const int tile0 = cb * NT;
+  const int m0 = mb * (MT * 16);
   const int per = (KT + KW - 1) / KW;
   const int kb = min(KT, wave * per);
   const int ke = min(KT, kb + per);
@@ -146,7 +163,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     }
   } else {
     // tiles (2p, 2p+1) = (gate, up) of output columns [16p, 16p+16)
-    int n = blockIdx.x * 16 + (lane & 15);
+    int n = cb * 16 + (lane & 15);
     if (n < N) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
@@ -163,10 +180,11 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 template <int MT, int NT, int KW, int U, int EPI, int MULTI>
 static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T, int N,
                       int K, int KT, int NTILES, int mpasses, hipStream_t s) {
-  dim3 grid((NTILES + NT - 1) / NT, mpasses);
+  const int ncb = (NTILES + NT - 1) / NT;
+  dim3 grid(MULTI ? (ncb + 7) / 8 * 8 * mpasses : ncb);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, MULTI>), grid, dim3(KW * 64), lds,
-                     s, X, Wp, Y, T, N, K, KT, NTILES);
+                     s, X, Wp, Y, T, N, K, KT, NTILES, MULTI ? mpasses : 1);
   return hipGetLastError();
 }
 
@@ -335,6 +353,175 @@ __global__ __launch_bounds__(256) void gemm_mid_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-DMA variant of the M-split kernel (the verify/prefill-chunk regime).
+// Both operands travel HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR
+// staging), through an NST-deep ring of stages.  One stage = one 32-deep
+// k-step: the 4 waves' own A fragments (4*MTW x 1 KiB, each wave loads its
+// MTW) + the NTW shared weight fragments (NTW/4 per wave).  The packed
+// weight fragment is already lane-linear (weights.hip), and an X fragment
+// is lane-linear by construction (lane l: row l&15, k 8(l>>4)..+7), so the
+// LDS image is read back with conflict-free ds_read_b128.  Waits are counted
+// (vmcnt = loads of the stages still allowed in flight) and the barrier is a
+// raw s_barrier, so NST-2 stages stay in flight across every barrier
+// (cdna_hip_programming.md §5 "Pipelining across barriers").
+// Same per-element reduction order as gemm_mid_kernel: MFMA chain over the
+// slice's k-steps, then slices in order.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(gsrc), "s"(lds_dst)
+      : "memory");
+}
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
+}
+// wait until at most G*ahead of this wave's DMA loads are outstanding
+template <int G, int A>
+__device__ __forceinline__ void vm_wait_stages(int ahead) {
+  if constexpr (A == 0) {
+    vm_wait<0>();
+  } else {
+    if (ahead >= A) vm_wait<G * A>();
+    else vm_wait_stages<G, A - 1>(ahead);
+  }
+}
+
+template <int MTW, int NTW, int EPI>
+__device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *__restrict__ Y,
+                                          float *__restrict__ Ypart, int T, int N, int NTILES,
+                                          int S, int ks, int tile0, int m0, int lane) {
+  // C/D layout: col = lane&15, row = (lane>>4)*4 + r
+  if (S > 1) {
+    const int NP = NTILES * 16;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int tile = tile0 + j;
+      if (tile >= NTILES) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Ypart[((size_t)ks * T + m) * NP + tile * 16 + (lane & 15)] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+  if (EPI == 0) {
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int n = (tile0 + j) * 16 + (lane & 15);
+      if (tile0 + j >= NTILES || n >= N) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
+        }
+    }
+  } else {
+#pragma unroll
+    for (int j = 0; j < NTW; j += 2) {
+      const int n = ((tile0 + j) >> 1) * 16 + (lane & 15);
+      if (tile0 + j >= NTILES || n >= N) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Y[(size_t)m * N + n] = silu_mul_h(acc[i][j][r], acc[i][j + 1][r]);
+        }
+    }
+  }
+}
+
+template <int MTW, int NTW, int NST, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(
+    const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
+    uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
+    int NTILES, int S) {
+  static_assert(NTW % 4 == 0, "NTW pieces are spread over 4 waves");
+  constexpr int PPT = NTW / 4;
+  constexpr int G = MTW + PPT;                   // DMA loads per wave per stage
+  constexpr int STAGE = (4 * MTW + NTW) * 1024;  // bytes per stage
+  static_assert(G * (NST - 2) <= 63, "vmcnt range");
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
+  const uint32_t lbase = (uint32_t)(uintptr_t)lds;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int tile0 = blockIdx.x * NTW;
+  const int ks = blockIdx.y;
+  const int m0 = blockIdx.z * (4 * MTW * 16) + wave * MTW * 16;
+  const int per = (KT + S - 1) / S;
+  const int kb = min(KT, ks * per);
+  const int ke = min(KT, kb + per);
+  const int nk = ke - kb;
+
+  const uint16_t *bsrc[PPT];
+#pragma unroll
+  for (int p = 0; p < PPT; ++p) {
+    const int t = min(tile0 + wave + 4 * p, NTILES - 1);
+    bsrc[p] = Wp + ((size_t)t * KT + kb) * 512 + lane * 8;
+  }
+  const uint16_t *xsrc[MTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i) {
+    const int r = min(m0 + i * 16 + (lane & 15), T - 1);
+    xsrc[i] = X + (size_t)r * K + kb * 32 + 8 * (lane >> 4);
+  }
+  // LDS addresses: stage s at s*STAGE; A of wave w at (w*MTW+i) KiB, B tile j at (4*MTW+j) KiB
+  const uint32_t a_dst = lbase + (uint32_t)(wave * MTW) * 1024u;
+  const uint32_t b_dst = lbase + (uint32_t)(4 * MTW + wave) * 1024u;
+  auto issue = [&](int st) {  // stage index st (relative to kb) -> ring slot st % NST
+    const uint32_t so = (uint32_t)(st % NST) * STAGE;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) glds16(xsrc[i] + st * 32, a_dst + so + i * 1024u);
+#pragma unroll
+    for (int p = 0; p < PPT; ++p) glds16(bsrc[p] + (size_t)st * 512, b_dst + so + p * 4096u);
+  };
+
+  f4 acc[MTW][NTW];
+#pragma unroll
+  for (int i = 0; i < MTW; ++i)
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+
+#pragma unroll
+  for (int st = 0; st < NST - 1; ++st)
+    if (st < nk) issue(st);
+  // (waves whose rows are all past T still run the MFMAs on clamped rows: a
+  // skip would put the accumulators through a phi and off the AGPRs)
+  for (int k = 0; k < nk; ++k) {
+    // stage k must have landed (this wave), then everyone's (barrier); the
+    // barrier also retires every wave's reads of stage k-1, whose slot the
+    // next issue overwrites
+    vm_wait_stages<G, NST - 2>(min(NST - 2, nk - 1 - k));
+    asm volatile("s_barrier" ::: "memory");
+    if (k + NST - 1 < nk) issue(k + NST - 1);
+    const char *sp = lds + (size_t)(k % NST) * STAGE;
+    h8 a[MTW], b[NTW];
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+      a[i] = *reinterpret_cast<const h8 *>(sp + (wave * MTW + i) * 1024 + lane * 16);
+#pragma unroll
+    for (int j = 0; j < NTW; ++j)
+      b[j] = *reinterpret_cast<const h8 *>(sp + (4 * MTW + j) * 1024 + lane * 16);
+#pragma unroll
+    for (int i = 0; i < MTW; ++i)
+#pragma unroll
+      for (int j = 0; j < NTW; ++j)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
+  }
+  mid_store<MTW, NTW, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0, m0, lane);
+}
+
 // Sum the S fp32 partial slabs in slice order, then the epilogue.
 template <int EPI>
 __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__restrict__ Y,
@@ -364,6 +551,8 @@ static int mid_split(int KT, int blocks) {
   return S > KT ? KT : S;
 }
 
+static int glds_split(int KT, int blocks);
+
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   const int mtiles = (T + 15) / 16;
   if (mtiles <= 4) return 0;
@@ -371,8 +560,60 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   const int MTW = mtiles <= 8 ? 2 : 3;
   const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
   const int nblk = (ntiles + 7) / 8;
-  const int S = mid_split(K / 32, nblk * mblocks);
+  const int S = std::max(mid_split(K / 32, nblk * mblocks), glds_split(K / 32, nblk * mblocks));
   return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
+}
+
+// k-split for the one-workgroup-per-CU DMA kernel: whole waves of 256
+// workgroups, ~8 k-steps of pipeline fill per workgroup.
+static int glds_split(int KT, int blocks) {
+  static const int force = getenv("FFMI_GEMM_S") ? atoi(getenv("FFMI_GEMM_S")) : 0;
+  if (force > 0) return force > KT ? KT : force;
+  int best = 1;
+  long bestc = -1;
+  for (int S = 1; S <= 8 && S <= KT; ++S) {
+    const long rounds = (blocks * (long)S + 255) / 256;
+    const long c = rounds * ((KT + S - 1) / S + 8) + (S > 1 ? 4 : 0);
+    if (bestc < 0 || c < bestc) best = S, bestc = c;
+  }
+  return best;
+}
+
+static bool use_glds() {
+  static const bool v = getenv("FFMI_GEMM_IMPL") && !strcmp(getenv("FFMI_GEMM_IMPL"), "glds");
+  return v;
+}
+
+template <int MTW, int NST>
+static hipError_t run_glds(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
+                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s) {
+  constexpr int NTW = 8;
+  const int KT = K / 32;
+  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
+  const int mtiles = (T + 15) / 16;
+  const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
+  const int nblk = (ntiles + NTW - 1) / NTW;
+  int S = glds_split(KT, nblk * mblocks);
+  const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
+  if (S > 1 && (!ws || ws_bytes < need)) S = 1;
+  dim3 grid(nblk, S, mblocks);
+  if (epi)
+    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NTW, NST, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws,
+                       T, N, K, KT, ntiles, S);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NTW, NST, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws,
+                       T, N, K, KT, ntiles, S);
+  if (S > 1) {
+    const long total = (long)T * N;
+    const unsigned blocks = (unsigned)((total + 255) / 256);
+    if (epi)
+      hipLaunchKernelGGL(gemm_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
+                         ntiles, S);
+    else
+      hipLaunchKernelGGL(gemm_reduce_kernel<0>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
+                         ntiles, S);
+  }
+  return hipGetLastError();
 }
 
 template <int MTW>
@@ -412,6 +653,24 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
   const int mtiles = (T + 15) / 16;
+  static const int mid_impl = [] {
+    const char *e = getenv("FFMI_GEMM_IMPL");
+    if (!e) return 0;
+    if (!strcmp(e, "skinny4")) return 4;
+    if (!strcmp(e, "skinny8")) return 8;
+    if (!strcmp(e, "skinny2")) return 2;
+    return 0;
+  }();
+  if (mtiles > 4 && mid_impl == 4)
+    return dispatch_nt<4, 4, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 3) / 4, s);
+  if (mtiles > 4 && mid_impl == 8)
+    return dispatch_nt<8, 2, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 7) / 8, s);
+  if (mtiles > 2 && mid_impl == 2)
+    return dispatch_nt<2, 8, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 1) / 2, s);
+  if (mtiles > 4 && use_glds()) {
+    if (mtiles > 8) return run_glds<3, 6>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
+    return run_glds<2, 7>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
+  }
   if (mtiles > 8) return run_mid<3>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
   if (mtiles > 4) return run_mid<2>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
   if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);

@@ -146,6 +146,7 @@ SIGNATURES = {
                                             ctypes.POINTER(c_void_p)]),
     "ffmi_status_str": (ctypes.c_char_p, [c_int]),
     "ffmi_version": (ctypes.c_char_p, []),
+    "ffmi_last_error": (ctypes.c_char_p, []),
 }
 
 _lib = None
@@ -164,8 +165,6 @@ def lib():
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
-        L.ffmi_last_error.restype = ctypes.c_char_p
-        L.ffmi_last_error.argtypes = []
         _lib = L
     return _lib
 

@@ -307,6 +307,8 @@ ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
                                         int disagree_pct, ffmi_model **out);
 
 const char *ffmi_status_str(ffmi_status s);
+/* message + file:line of the last failing check on this process */
+const char *ffmi_last_error(void);
 const char *ffmi_version(void);
 
 #ifdef __cplusplus

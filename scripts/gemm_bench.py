@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--shapes", default="llama7b")
     ap.add_argument("--T", default="1,8,24,64,168,192")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--cold-mb", type=int, default=768,
+                    help="rotate weight copies totalling this many MB (0: one hot copy)")
     args = ap.parse_args()
     L = F.lib()
     rng = np.random.default_rng(0)
@@ -46,22 +48,31 @@ def main():
         else:
             F.check(L.ffmi_linear_pack_weight(src.ptr, N, K, Wp.ptr, None))
         del src
+        # copies so that one rotation exceeds the 256 MB last-level cache
+        ncopy = max(1, -(-args.cold_mb * (1 << 20) // nb)) if args.cold_mb else 1
+        Wps = [Wp]
+        for _ in range(ncopy - 1):
+            c = Buf.empty((nb // 2,), np.uint16)
+            assert hip().hipMemcpy(c.ptr, Wp.ptr, nb, 3) == 0
+            Wps.append(c)
         for T in [int(t) for t in args.T.split(",")]:
-            X = Buf(f16(rng.standard_normal((T, K))))
+            Xs = [Buf(f16(rng.standard_normal((T, K)))) for _ in range(len(Wps))]
             Y = Buf.empty((T, N), np.float16)
-            for _ in range(3):
-                F.check(L.ffmi_linear(X.ptr, Wp.ptr, Y.ptr, T, N, K, epi, None))
+            for i in range(len(Wps)):
+                F.check(L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi, None))
             tm = Timer()
             tm.start()
-            for _ in range(args.iters):
-                L.ffmi_linear(X.ptr, Wp.ptr, Y.ptr, T, N, K, epi, None)
+            for it in range(args.iters):
+                i = it % len(Wps)
+                L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi, None)
             ms = tm.stop() / args.iters
             byts = 2.0 * (rows * K + T * K + T * N)
-            r = dict(op=name, T=T, N=N, K=K, us=round(ms * 1e3, 2),
+            r = dict(op=name, T=T, N=N, K=K, copies=len(Wps), us=round(ms * 1e3, 2),
                      GBps=round(byts / (ms * 1e-3) / 1e9, 1),
                      TFLOPs=round(2.0 * T * rows * K / (ms * 1e-3) / 1e12, 1))
             res.append(r)
             print(json.dumps(r), flush=True)
+        del Wps, Wp
     return res
 
 

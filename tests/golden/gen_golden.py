@@ -87,7 +87,8 @@ def build_hf(cfg):
 
 
 def make_prompt(cfg):
-    # BOS(1) + ids from splitmix64 -- same generator as bench.py's prompts
+    # BOS(1) + ids uniform in [3, vocab) from numpy default_rng(seed) (bench.py
+    # uses splitmix64 for its 128-token prompts; fixtures only need determinism)
     rng = np.random.default_rng(cfg["seed"])
     ids = rng.integers(3, cfg["vocab_size"], size=cfg["prompt_len"] - 1)
     return np.concatenate([[1], ids]).astype(np.int32)
