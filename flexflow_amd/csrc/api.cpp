@@ -163,6 +163,9 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   FFMI_CHECK(cfg->num_heads > 0 && cfg->max_requests > 0 && cfg->max_seq_len > 0 &&
                  cfg->max_tokens > 0,
              FFMI_ERR_INVALID);
+  FFMI_CHECK(cfg->out_layout == 0 || cfg->out_layout == 1, FFMI_ERR_INVALID);
+  FFMI_CHECK(cfg->out_layout == 0 || (cfg->num_heads * cfg->head_dim) % 32 == 0,
+             FFMI_ERR_UNSUPPORTED);
   ffmi_attn *h = new ffmi_attn();
   h->cfg = *cfg;
   h->slots = (cfg->max_seq_len + cfg->max_tree_tokens + 31) & ~31;
@@ -222,7 +225,8 @@ static ffmi_status attn_run(ffmi_attn *h, const ffmi_batch_dev *b, const void *q
                                    h->vc, tree ? h->stage : nullptr, h->rope, heads, d, h->slots,
                                    h->slots, s));
   FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, h->qbuf, h->kc, h->vc, (uint16_t *)out,
-                                  heads, d, h->slots, h->cfg.qk_scale, s));
+                                  heads, d, h->slots, h->cfg.qk_scale, s,
+                                  h->cfg.out_layout == 1));
   return FFMI_OK;
 }
 
@@ -276,7 +280,10 @@ extern "C" ffmi_status ffmi_linear_ws(const void *X, const void *W_packed, void 
                                       size_t workspace_bytes, ffmi_stream stream) {
   FFMI_CHECK(X && W_packed && Y && T >= 0 && out_dim > 0, FFMI_ERR_INVALID);
   FFMI_CHECK(in_dim > 0 && in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
-  FFMI_CHECK(epilogue == FFMI_EPI_NONE || epilogue == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
+  const int epi = epilogue & ~FFMI_X_PACKED;
+  const int epi_base = epi & ~FFMI_Y_PACKED;
+  FFMI_CHECK(epi_base == FFMI_EPI_NONE || epi_base == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
+  FFMI_CHECK(!(epilogue & FFMI_Y_PACKED) || out_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
   FFMI_HIP(ffmi::launch_gemm((const uint16_t *)X, (const uint16_t *)W_packed, (uint16_t *)Y,
                              (float *)workspace, workspace_bytes, T, out_dim, in_dim, epilogue,
                              (hipStream_t)stream));
@@ -325,6 +332,20 @@ extern "C" ffmi_status ffmi_residual_rmsnorm(const void *x1, const void *x2, con
   FFMI_HIP(ffmi::launch_rmsnorm((const uint16_t *)x1, (const uint16_t *)x2, (const uint16_t *)w,
                                 (uint16_t *)residual_out, (uint16_t *)out, T, H, eps,
                                 (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rmsnorm_ex(const void *x1, const void *x2, const void *w,
+                                       void *residual_out, void *out, int T, int H, float eps,
+                                       int flags, ffmi_stream stream) {
+  FFMI_CHECK(x1 && w && out && T >= 0 && H > 0 && H % 8 == 0, FFMI_ERR_INVALID);
+  FFMI_CHECK(!x2 || residual_out, FFMI_ERR_INVALID);
+  FFMI_CHECK((flags & ~FFMI_Y_PACKED) == 0, FFMI_ERR_INVALID);
+  const bool packed = (flags & FFMI_Y_PACKED) != 0;
+  FFMI_CHECK(!packed || H % 32 == 0, FFMI_ERR_UNSUPPORTED);
+  FFMI_HIP(ffmi::launch_rmsnorm((const uint16_t *)x1, (const uint16_t *)x2, (const uint16_t *)w,
+                                (uint16_t *)residual_out, (uint16_t *)out, T, H, eps,
+                                (hipStream_t)stream, packed));
   return FFMI_OK;
 }
 
@@ -425,5 +446,22 @@ extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, s
     ffmi_set_last_error(ncclGetErrorString(r), __FILE__, __LINE__);
     return FFMI_ERR_NCCL;
   }
+  return FFMI_OK;
+}
+
+extern "C" long ffmi_debug_gemm_stamps(long long *dst, long max_waves) {
+  return ffmi::gemm_debug_stamps(dst, max_waves);
+}
+
+extern "C" size_t ffmi_packed_activation_bytes(int T, int in_dim) {
+  return T > 0 && in_dim > 0 ? ffmi::packed_act_bytes(T, in_dim) : 0;
+}
+
+extern "C" ffmi_status ffmi_pack_activations(const void *X, int T, int in_dim, void *X_packed,
+                                             ffmi_stream stream) {
+  FFMI_CHECK(X && X_packed && T >= 0 && in_dim > 0, FFMI_ERR_INVALID);
+  FFMI_CHECK(in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
+  FFMI_HIP(ffmi::launch_pack_act((const uint16_t *)X, (uint16_t *)X_packed, T, in_dim,
+                                 (hipStream_t)stream));
   return FFMI_OK;
 }

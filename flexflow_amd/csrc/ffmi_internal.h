@@ -31,6 +31,17 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// Packed activation tiles (FFMI_X_PACKED / FFMI_Y_PACKED): element (m, n) of a
+// [T][K] activation lives at [m/16][n/32][lane = (m&15) + 16*((n>>3)&3)][n&7],
+// i.e. each 16-row x 32-column block is one MFMA operand fragment (1 KiB,
+// lane-linear), the same order the weights are packed in (weights.hip).
+__host__ __device__ __forceinline__ size_t act_packed_off(int m, int n, int K) {
+  return ((((size_t)(m >> 4) * (size_t)(K >> 5) + (size_t)(n >> 5)) * 64 + (m & 15) +
+           16 * ((n >> 3) & 3))
+          << 3) +
+         (n & 7);
+}
+
 // Layout of the packed per-step metadata blob (device copy of ffmi_batch_desc).
 struct BatchHeader {
   int32_t num_tokens, num_work, num_commits, num_mask_reqs;
@@ -64,9 +75,12 @@ hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
+long gemm_debug_stamps(long long *dst, long max_waves);
+size_t packed_act_bytes(int T, int K);
+hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s);
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s);
+                          hipStream_t s, bool out_packed = false);
 hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
                             uint16_t *out, int H, hipStream_t s);
 hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
@@ -82,7 +96,8 @@ hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
                          hipStream_t s);
 hipError_t launch_attention(const char *blob, int W, const uint16_t *qbuf,
                             const uint16_t *kc, const uint16_t *vc, uint16_t *out,
-                            int heads, int d, int slots, float scale, hipStream_t s);
+                            int heads, int d, int slots, float scale, hipStream_t s,
+                            bool out_packed = false);
 
 uint64_t weight_key(const char *name, uint64_t seed);
 

@@ -142,7 +142,7 @@ template <int D>
 __global__ __launch_bounds__(256) void attention_kernel(
     const char *__restrict__ blob, const uint16_t *__restrict__ qbuf,
     const uint16_t *__restrict__ kc, const uint16_t *__restrict__ vc,
-    uint16_t *__restrict__ out, int heads, int slots, float scale) {
+    uint16_t *__restrict__ out, int heads, int slots, float scale, int out_packed) {
   constexpr int KS = D / 32;  // k-steps of the QK^T product
   constexpr int DT = D / 16;  // d-tiles of the PV product
   __shared__ float sm_m[4][16];
@@ -264,7 +264,8 @@ __global__ __launch_bounds__(256) void attention_kernel(
   }
   const float inv = 1.0f / (L + 1e-6f);
   if (!qvalid) return;
-  uint16_t *orow = out + (size_t)(w.q_start + qi) * Hl + h * D;
+  const int orow_m = w.q_start + qi;
+  uint16_t *orow = out + (size_t)orow_m * Hl + h * D;
   for (int t = wave; t < DT; t += 4) {
     uint16_t r4[4];
 #pragma unroll
@@ -277,21 +278,25 @@ __global__ __launch_bounds__(256) void attention_kernel(
     uint2 pk;
     pk.x = r4[0] | ((uint32_t)r4[1] << 16);
     pk.y = r4[2] | ((uint32_t)r4[3] << 16);
-    *reinterpret_cast<uint2 *>(orow + t * 16 + 4 * g) = pk;
+    uint16_t *dst = out_packed ? out + act_packed_off(orow_m, h * D + t * 16 + 4 * g, Hl)
+                               : orow + t * 16 + 4 * g;
+    *reinterpret_cast<uint2 *>(dst) = pk;
   }
 }
 
 hipError_t launch_attention(const char *blob, int W, const uint16_t *qbuf, const uint16_t *kc,
                             const uint16_t *vc, uint16_t *out, int heads, int d, int slots,
-                            float scale, hipStream_t s) {
+                            float scale, hipStream_t s, bool out_packed) {
   if (W <= 0) return hipSuccess;
+  if (out_packed && (heads * d) % 32) return hipErrorInvalidValue;
+  const int op = out_packed ? 1 : 0;
   dim3 grid(W, heads);
   if (d == 128)
     hipLaunchKernelGGL(attention_kernel<128>, grid, dim3(256), 0, s, blob, qbuf, kc, vc, out,
-                       heads, slots, scale);
+                       heads, slots, scale, op);
   else if (d == 64)
     hipLaunchKernelGGL(attention_kernel<64>, grid, dim3(256), 0, s, blob, qbuf, kc, vc, out,
-                       heads, slots, scale);
+                       heads, slots, scale, op);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();

@@ -24,10 +24,24 @@
 #include <string.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "../ffmi_internal.h"
 
 namespace ffmi {
+
+// compile-time loop: f(std::integral_constant<int, 0>) ... f(<N-1>)
+template <int I, int N, class F>
+__device__ __forceinline__ void static_for_impl(F &&f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for_impl<I + 1, N>(f);
+  }
+}
+template <int N, class F>
+__device__ __forceinline__ void static_for(F &&f) {
+  static_for_impl<0, N>(f);
+}
 
 // SigmoidSiluMultiKernel numerics (sigmoid_silu_multi.cu:41-46): gate and up
 // are fp16 values, out = half(half(g * half(sigmoid(g))) * u)
@@ -48,7 +62,8 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
 template <int MT, int NT, int KW, int U, int EPI, int MULTI>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *__restrict__ Y, int T, int N, int K, int KT, int NTILES, int mpasses) {
+    uint16_t *__restrict__ Y, int T, int N, int K, int KT, int NTILES, int mpasses, int xp,
+    int yp) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -72,11 +87,18 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 #pragma unroll
     for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // X row-major, or packed activation tiles (xp): 1 KiB per fragment load
+  const int XS = xp ? 512 : 32;
   const uint16_t *xrow[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) {
-    int r = min(m0 + i * 16 + (lane & 15), T - 1);
-    xrow[i] = X + (size_t)r * K + 8 * (lane >> 4);
+    if (xp) {
+      const int mt = min((m0 + i * 16) >> 4, (T - 1) >> 4);
+      xrow[i] = X + ((size_t)mt * KT * 64 + lane) * 8;
+    } else {
+      const int r = min(m0 + i * 16 + (lane & 15), T - 1);
+      xrow[i] = X + (size_t)r * K + 8 * (lane >> 4);
+    }
   }
   const uint16_t *wrow[NT];
 #pragma unroll
@@ -98,7 +120,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int i = 0; i < MT; ++i)
-        a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (kt + u) * 32);
+        a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)(kt + u) * XS);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -115,7 +137,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
       b[j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)kt * 512);
 #pragma unroll
     for (int i = 0; i < MT; ++i) {
-      h8 a = *reinterpret_cast<const h8 *>(xrow[i] + kt * 32);
+      h8 a = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kt * XS);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
@@ -158,7 +180,9 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
+          if (m < T)
+            Y[yp ? act_packed_off(m, n, N) : (size_t)m * N + n] =
+                __half_as_ushort(__float2half_rn(acc[i][j][r]));
         }
     }
   } else {
@@ -171,7 +195,8 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         for (int r = 0; r < 4; ++r) {
           int m = m0 + i * 16 + (lane >> 4) * 4 + r;
           if (m >= T) continue;
-          Y[(size_t)m * N + n] = silu_mul_h(acc[i][0][r], acc[i][1][r]);
+          Y[yp ? act_packed_off(m, n, N) : (size_t)m * N + n] =
+              silu_mul_h(acc[i][0][r], acc[i][1][r]);
         }
     }
   }
@@ -179,27 +204,28 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 
 template <int MT, int NT, int KW, int U, int EPI, int MULTI>
 static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T, int N,
-                      int K, int KT, int NTILES, int mpasses, hipStream_t s) {
+                      int K, int KT, int NTILES, int mpasses, hipStream_t s, int xp, int yp) {
   const int ncb = (NTILES + NT - 1) / NT;
   dim3 grid(MULTI ? (ncb + 7) / 8 * 8 * mpasses : ncb);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, MULTI>), grid, dim3(KW * 64), lds,
-                     s, X, Wp, Y, T, N, K, KT, NTILES, MULTI ? mpasses : 1);
+                     s, X, Wp, Y, T, N, K, KT, NTILES, MULTI ? mpasses : 1, xp, yp);
   return hipGetLastError();
 }
 
 template <int MT, int U, int MULTI>
 static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T,
-                              int N, int K, int KT, int epi, int mpasses, hipStream_t s) {
+                              int N, int K, int KT, int epi, int mpasses, hipStream_t s,
+                              int xp = 0, int yp = 0) {
   int ntiles = (N + 15) / 16;
   if (epi == FFMI_EPI_SILU_MUL)
-    return run<MT, 2, 4, U, 1, MULTI>(X, Wp, Y, T, N, K, KT, 2 * ntiles, mpasses, s);
+    return run<MT, 2, 4, U, 1, MULTI>(X, Wp, Y, T, N, K, KT, 2 * ntiles, mpasses, s, xp, yp);
   if (MT >= 4 && ntiles >= 512)
-    return run<MT, 2, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s);
+    return run<MT, 2, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
   // 8-wave groups only where the accumulators fit 2 waves/SIMD (no spills)
   if (ntiles >= 512 || MT >= 8)
-    return run<MT, 1, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s);
-  return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s);
+    return run<MT, 1, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
+  return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
 }
 
 // ---------------------------------------------------------------------------
@@ -217,12 +243,74 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
 // the 256 CUs.  Reduction order per output element: MFMA chain over the
 // slice's k-steps, then slices 0..S-1 -- fixed by (N, K, S), not by T.
 // ---------------------------------------------------------------------------
+// Epilogue of the M-split kernel.  Its MFMAs compute D = W_tile . X_tile^T,
+// so a lane's accumulator holds FOUR CONSECUTIVE OUTPUT COLUMNS
+// n = tile*16 + (lane>>4)*4 + r of one row m = m0 + i*16 + (lane&15): the
+// fp16 output goes out as one 8-byte store and an fp32 partial as one 16-byte
+// store per (i, j) (scalar 2-/4-byte stores in the C layout were the
+// kernel's single largest cost).
 template <int MTW, int NTW, int EPI>
-__global__ __launch_bounds__(256) void gemm_mid_kernel(
+__device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *__restrict__ Y,
+                                          float *__restrict__ Ypart, int T, int N, int NTILES,
+                                          int S, int ks, int tile0, int m0, int lane, int yp) {
+  const int mr = lane & 15, nq = (lane >> 4) * 4;
+  if (S > 1) {
+    const int NP = NTILES * 16;
+#pragma unroll
+    for (int j = 0; j < NTW; ++j) {
+      const int tile = tile0 + j;
+      if (tile >= NTILES) continue;
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) {
+        const int m = m0 + i * 16 + mr;
+        if (m < T)
+          *reinterpret_cast<f4 *>(Ypart + ((size_t)ks * T + m) * NP + tile * 16 + nq) = acc[i][j];
+      }
+    }
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < NTW; j += (EPI ? 2 : 1)) {
+    const int tile = tile0 + j;
+    if (tile >= NTILES) continue;
+    const int n = (EPI ? (tile >> 1) : tile) * 16 + nq;
+    if (n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < MTW; ++i) {
+      const int m = m0 + i * 16 + mr;
+      if (m >= T) continue;
+      uint16_t o[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        o[r] = EPI ? silu_mul_h(acc[i][j][r], acc[i][j + 1][r])
+                   : __half_as_ushort(__float2half_rn(acc[i][j][r]));
+      uint16_t *dst = yp ? Y + act_packed_off(m, n, N) : Y + (size_t)m * N + n;
+      if (n + 4 <= N && (((uintptr_t)dst & 7) == 0)) {
+        *reinterpret_cast<uint2 *>(dst) =
+            make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
+      } else {
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (n + r < N) dst[r] = o[r];
+      }
+    }
+  }
+}
+
+// Diagnostic stamps (FFMI_GEMM_STAMP=1 builds only): per wave
+// {realtime start, after prologue, after k-loop, end, HW_ID, XCC_ID}, 100 MHz.
+__device__ long long *g_gemm_stamps;
+__device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
+
+template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false>
+__global__ __launch_bounds__(256, 2) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
-    int NTILES, int S) {
+    int NTILES, int S, int yp) {
+  long long st0 = 0, st1 = 0, st2 = 0;
+  if (STAMP) st0 = rt_now();
   static_assert(NTW % 4 == 0, "NTW pieces are spread over 4 waves");
+  static_assert(PF >= 2, "ring depth");
   constexpr int PPT = NTW / 4;
   __shared__ __attribute__((aligned(16))) h8 sB[2][NTW][64];
   const int lane = threadIdx.x & 63;
@@ -242,11 +330,19 @@ __global__ __launch_bounds__(256) void gemm_mid_kernel(
     const int t = min(tile0 + bj[p], NTILES - 1);
     bsrc[p] = Wp + (size_t)t * KT * 512 + lane * 8;
   }
+  // X row-major [T][K] (16 rows x 64 B per fragment load), or XP: packed
+  // activation tiles [T/16][KT][64 lanes][8] (one contiguous 1 KiB per load)
+  constexpr int XS = XP ? 512 : 32;  // halves per k-step
   const uint16_t *xrow[MTW];
 #pragma unroll
   for (int i = 0; i < MTW; ++i) {
-    const int r = min(m0 + i * 16 + (lane & 15), T - 1);
-    xrow[i] = X + (size_t)r * K + 8 * (lane >> 4);
+    if (XP) {
+      const int mt = min((m0 + i * 16) >> 4, (T - 1) >> 4);
+      xrow[i] = X + ((size_t)mt * KT * 64 + lane) * 8;
+    } else {
+      const int r = min(m0 + i * 16 + (lane & 15), T - 1);
+      xrow[i] = X + (size_t)r * K + 8 * (lane >> 4);
+    }
   }
   f4 acc[MTW][NTW];
 #pragma unroll
@@ -254,294 +350,124 @@ __global__ __launch_bounds__(256) void gemm_mid_kernel(
 #pragma unroll
     for (int j = 0; j < NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
 
-  // Software pipeline (per k-step: one barrier, weight tile double-buffered
-  // in LDS).  Weight loads run PF=3 k-steps ahead in a register ring, X
-  // fragments one step ahead; X(k+1) is issued BEFORE B(k+3) so that the
-  // in-order vmcnt wait for X(k+1) never forces the younger weight loads.
+  // Software pipeline, one barrier per 32-deep k-step.  A PF-deep register
+  // ring holds BOTH operands of k-steps k..k+PF-1: slot q = (X(k), B(k)).
+  // Loads retire in issue order (vmcnt), so X must be issued as early as the
+  // weights: X(k) is consumed PF steps after issue, B(k+1) goes to the LDS
+  // tile PF-1 steps after issue, and no consumer waits on a young load.
   if (kb < ke) {
-    constexpr int PF = 3;
     h8 bq[PF][PPT];
-    h8 a[MTW], an[MTW];
+    h8 xq[PF][MTW];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int kq = min(kb + q, ke - 1);
+#pragma unroll
+      for (int i = 0; i < MTW; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
         bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
     }
 #pragma unroll
-    for (int i = 0; i < MTW; ++i) a[i] = *reinterpret_cast<const h8 *>(xrow[i] + kb * 32);
-#pragma unroll
     for (int p = 0; p < PPT; ++p) sB[0][bj[p]][lane] = bq[0][p];
     __syncthreads();
+    if (STAMP) st1 = rt_now();
+    // one k-step on ring slot Q; MFMAs read the slot in place, then it is
+    // refilled (a copy would rotate the ring through fresh registers and
+    // force vmcnt drains at the loop back-edge)
     int cur = 0;
-    for (int kt0 = kb; kt0 < ke; kt0 += PF) {
+    auto step = [&](auto Qc, int kt) {
+      constexpr int Q = decltype(Qc)::value;
+      h8 b[NTW];
 #pragma unroll
-      for (int q = 0; q < PF; ++q) {
-        const int kt = kt0 + q;
-        if (kt >= ke) break;
-        const int kx = min(kt + 1, ke - 1);
+      for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
 #pragma unroll
-        for (int i = 0; i < MTW; ++i) an[i] = *reinterpret_cast<const h8 *>(xrow[i] + kx * 32);
-        // slot q held B(kt); it is free once B(kt) went to LDS (previous step)
-        const int kw = min(kt + PF, ke - 1);
-        h8 b[NTW];
+      for (int i = 0; i < MTW; ++i)
 #pragma unroll
-        for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
+        for (int j = 0; j < NTW; ++j)  // D = W . X^T (see mid_store)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], xq[Q][i], acc[i][j], 0, 0, 0);
+      const int kw = min(kt + PF, ke - 1);
 #pragma unroll
-        for (int p = 0; p < PPT; ++p)
-          bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
+      for (int i = 0; i < MTW; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
-        for (int i = 0; i < MTW; ++i)
+      for (int p = 0; p < PPT; ++p)
+        bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
+      // B(kt+1) lives in ring slot (Q+1) % PF
 #pragma unroll
-          for (int j = 0; j < NTW; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-        // B(kt+1) lives in ring slot (q+1) % PF
-#pragma unroll
-        for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bq[(q + 1) % PF][p];
-        __syncthreads();
-#pragma unroll
-        for (int i = 0; i < MTW; ++i) a[i] = an[i];
-        cur ^= 1;
-      }
-    }
+      for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bq[(Q + 1) % PF][p];
+      __syncthreads();
+      cur ^= 1;
+    };
+    int kt0 = kb;
+    for (; kt0 + PF <= ke; kt0 += PF)  // steady state: whole ring turns
+      static_for<PF>([&](auto Qc) { step(Qc, kt0 + decltype(Qc)::value); });
+    static_for<PF - 1>([&](auto Qc) {  // tail: < PF steps, slots 0..
+      if (kt0 + decltype(Qc)::value < ke) step(Qc, kt0 + decltype(Qc)::value);
+    });
   }
+  if (STAMP) st2 = rt_now();
 
-  // C/D layout: col = lane&15, row = (lane>>4)*4 + r
-  if (S > 1) {
-    const int NP = NTILES * 16;
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int tile = tile0 + j;
-      if (tile >= NTILES) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Ypart[((size_t)ks * T + m) * NP + tile * 16 + (lane & 15)] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  if (EPI == 0) {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n = (tile0 + j) * 16 + (lane & 15);
-      if (tile0 + j >= NTILES || n >= N) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
-        }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < NTW; j += 2) {
-      const int n = ((tile0 + j) >> 1) * 16 + (lane & 15);
-      if (tile0 + j >= NTILES || n >= N) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Y[(size_t)m * N + n] = silu_mul_h(acc[i][j][r], acc[i][j + 1][r]);
-        }
+  mid_store<MTW, NTW, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0, m0, lane, yp);
+  if (STAMP) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const long long st3 = rt_now();
+    unsigned hwid, xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    if (lane == 0 && g_gemm_stamps) {
+      const long b = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
+      long long *d = g_gemm_stamps + (b * 4 + wave) * 6;
+      d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = hwid; d[5] = xcc;
     }
   }
 }
 
-// ---------------------------------------------------------------------------
-// LDS-DMA variant of the M-split kernel (the verify/prefill-chunk regime).
-// Both operands travel HBM/L2 -> LDS by global_load_lds_dwordx4 (no VGPR
-// staging), through an NST-deep ring of stages.  One stage = one 32-deep
-// k-step: the 4 waves' own A fragments (4*MTW x 1 KiB, each wave loads its
-// MTW) + the NTW shared weight fragments (NTW/4 per wave).  The packed
-// weight fragment is already lane-linear (weights.hip), and an X fragment
-// is lane-linear by construction (lane l: row l&15, k 8(l>>4)..+7), so the
-// LDS image is read back with conflict-free ds_read_b128.  Waits are counted
-// (vmcnt = loads of the stages still allowed in flight) and the barrier is a
-// raw s_barrier, so NST-2 stages stay in flight across every barrier
-// (cdna_hip_programming.md §5 "Pipelining across barriers").
-// Same per-element reduction order as gemm_mid_kernel: MFMA chain over the
-// slice's k-steps, then slices in order.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ void glds16(const void *gsrc, uint32_t lds_dst) {
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(gsrc), "s"(lds_dst)
-      : "memory");
+static long long *stamp_buf() {
+  static long long *buf = nullptr;
+  if (!buf) {
+    if (hipMalloc(&buf, (size_t)8 << 20) != hipSuccess) return nullptr;
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_gemm_stamps), &buf, sizeof(buf));
+  }
+  return buf;
 }
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  asm volatile("s_waitcnt vmcnt(%0)" ::"i"(N) : "memory");
-}
-// wait until at most G*ahead of this wave's DMA loads are outstanding
-template <int G, int A>
-__device__ __forceinline__ void vm_wait_stages(int ahead) {
-  if constexpr (A == 0) {
-    vm_wait<0>();
-  } else {
-    if (ahead >= A) vm_wait<G * A>();
-    else vm_wait_stages<G, A - 1>(ahead);
-  }
-}
+static long g_stamp_entries = 0;
 
-template <int MTW, int NTW, int EPI>
-__device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *__restrict__ Y,
-                                          float *__restrict__ Ypart, int T, int N, int NTILES,
-                                          int S, int ks, int tile0, int m0, int lane) {
-  // C/D layout: col = lane&15, row = (lane>>4)*4 + r
-  if (S > 1) {
-    const int NP = NTILES * 16;
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int tile = tile0 + j;
-      if (tile >= NTILES) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Ypart[((size_t)ks * T + m) * NP + tile * 16 + (lane & 15)] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-  if (EPI == 0) {
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) {
-      const int n = (tile0 + j) * 16 + (lane & 15);
-      if (tile0 + j >= NTILES || n >= N) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Y[(size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
-        }
-    }
-  } else {
-#pragma unroll
-    for (int j = 0; j < NTW; j += 2) {
-      const int n = ((tile0 + j) >> 1) * 16 + (lane & 15);
-      if (tile0 + j >= NTILES || n >= N) continue;
-#pragma unroll
-      for (int i = 0; i < MTW; ++i)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          if (m < T) Y[(size_t)m * N + n] = silu_mul_h(acc[i][j][r], acc[i][j + 1][r]);
-        }
-    }
-  }
-}
 
-template <int MTW, int NTW, int NST, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_glds_kernel(
-    const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
-    int NTILES, int S) {
-  static_assert(NTW % 4 == 0, "NTW pieces are spread over 4 waves");
-  constexpr int PPT = NTW / 4;
-  constexpr int G = MTW + PPT;                   // DMA loads per wave per stage
-  constexpr int STAGE = (4 * MTW + NTW) * 1024;  // bytes per stage
-  static_assert(G * (NST - 2) <= 63, "vmcnt range");
-  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE];
-  const uint32_t lbase = (uint32_t)(uintptr_t)lds;
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int tile0 = blockIdx.x * NTW;
-  const int ks = blockIdx.y;
-  const int m0 = blockIdx.z * (4 * MTW * 16) + wave * MTW * 16;
-  const int per = (KT + S - 1) / S;
-  const int kb = min(KT, ks * per);
-  const int ke = min(KT, kb + per);
-  const int nk = ke - kb;
-
-  const uint16_t *bsrc[PPT];
-#pragma unroll
-  for (int p = 0; p < PPT; ++p) {
-    const int t = min(tile0 + wave + 4 * p, NTILES - 1);
-    bsrc[p] = Wp + ((size_t)t * KT + kb) * 512 + lane * 8;
-  }
-  const uint16_t *xsrc[MTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i) {
-    const int r = min(m0 + i * 16 + (lane & 15), T - 1);
-    xsrc[i] = X + (size_t)r * K + kb * 32 + 8 * (lane >> 4);
-  }
-  // LDS addresses: stage s at s*STAGE; A of wave w at (w*MTW+i) KiB, B tile j at (4*MTW+j) KiB
-  const uint32_t a_dst = lbase + (uint32_t)(wave * MTW) * 1024u;
-  const uint32_t b_dst = lbase + (uint32_t)(4 * MTW + wave) * 1024u;
-  auto issue = [&](int st) {  // stage index st (relative to kb) -> ring slot st % NST
-    const uint32_t so = (uint32_t)(st % NST) * STAGE;
-#pragma unroll
-    for (int i = 0; i < MTW; ++i) glds16(xsrc[i] + st * 32, a_dst + so + i * 1024u);
-#pragma unroll
-    for (int p = 0; p < PPT; ++p) glds16(bsrc[p] + (size_t)st * 512, b_dst + so + p * 4096u);
-  };
-
-  f4 acc[MTW][NTW];
-#pragma unroll
-  for (int i = 0; i < MTW; ++i)
-#pragma unroll
-    for (int j = 0; j < NTW; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-
-#pragma unroll
-  for (int st = 0; st < NST - 1; ++st)
-    if (st < nk) issue(st);
-  // (waves whose rows are all past T still run the MFMAs on clamped rows: a
-  // skip would put the accumulators through a phi and off the AGPRs)
-  for (int k = 0; k < nk; ++k) {
-    // stage k must have landed (this wave), then everyone's (barrier); the
-    // barrier also retires every wave's reads of stage k-1, whose slot the
-    // next issue overwrites
-    vm_wait_stages<G, NST - 2>(min(NST - 2, nk - 1 - k));
-    asm volatile("s_barrier" ::: "memory");
-    if (k + NST - 1 < nk) issue(k + NST - 1);
-    const char *sp = lds + (size_t)(k % NST) * STAGE;
-    h8 a[MTW], b[NTW];
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-      a[i] = *reinterpret_cast<const h8 *>(sp + (wave * MTW + i) * 1024 + lane * 16);
-#pragma unroll
-    for (int j = 0; j < NTW; ++j)
-      b[j] = *reinterpret_cast<const h8 *>(sp + (4 * MTW + j) * 1024 + lane * 16);
-#pragma unroll
-    for (int i = 0; i < MTW; ++i)
-#pragma unroll
-      for (int j = 0; j < NTW; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[i], b[j], acc[i][j], 0, 0, 0);
-  }
-  mid_store<MTW, NTW, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0, m0, lane);
-}
-
-// Sum the S fp32 partial slabs in slice order, then the epilogue.
+// Sum the S fp32 partial slabs in slice order, then the epilogue; one thread
+// per 4 consecutive output columns (16-B slab loads, 8-B fp16 store).
 template <int EPI>
 __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__restrict__ Y,
-                                   int T, int N, int NTILES, int S) {
+                                   int T, int N, int NTILES, int S, int yp) {
   const int NP = NTILES * 16;
+  const int nq = (N + 3) / 4;
   const long idx = blockIdx.x * (long)blockDim.x + threadIdx.x;
-  if (idx >= (long)T * N) return;
-  const int m = (int)(idx / N), n = (int)(idx % N);
+  if (idx >= (long)T * nq) return;
+  const int m = (int)(idx / nq), n = (int)(idx % nq) * 4;
+  const size_t slab = (size_t)T * NP;
+  f4 acc, up;
   if (EPI == 0) {
-    float acc = Ypart[(size_t)m * NP + n];
-    for (int s = 1; s < S; ++s) acc += Ypart[((size_t)s * T + m) * NP + n];
-    Y[idx] = __half_as_ushort(__float2half_rn(acc));
+    const float *src = Ypart + (size_t)m * NP + n;
+    acc = *reinterpret_cast<const f4 *>(src);
+    for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f4 *>(src + s * slab);
   } else {
-    const int gcol = (n >> 4) * 32 + (n & 15);
-    float g = Ypart[(size_t)m * NP + gcol], u = Ypart[(size_t)m * NP + gcol + 16];
+    const float *src = Ypart + (size_t)m * NP + (n >> 4) * 32 + (n & 15);
+    acc = *reinterpret_cast<const f4 *>(src);
+    up = *reinterpret_cast<const f4 *>(src + 16);
     for (int s = 1; s < S; ++s) {
-      g += Ypart[((size_t)s * T + m) * NP + gcol];
-      u += Ypart[((size_t)s * T + m) * NP + gcol + 16];
+      acc += *reinterpret_cast<const f4 *>(src + s * slab);
+      up += *reinterpret_cast<const f4 *>(src + s * slab + 16);
     }
-    Y[idx] = silu_mul_h(g, u);
+  }
+  uint16_t o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+    o[r] = EPI ? silu_mul_h(acc[r], up[r]) : __half_as_ushort(__float2half_rn(acc[r]));
+  uint16_t *dst = yp ? Y + act_packed_off(m, n, N) : Y + (size_t)m * N + n;
+  if (n + 4 <= N && (((uintptr_t)dst & 7) == 0)) {
+    *reinterpret_cast<uint2 *>(dst) =
+        make_uint2(o[0] | ((uint32_t)o[1] << 16), o[2] | ((uint32_t)o[3] << 16));
+  } else {
+    for (int r = 0; r < 4; ++r)
+      if (n + r < N) dst[r] = o[r];
   }
 }
 
@@ -551,74 +477,22 @@ static int mid_split(int KT, int blocks) {
   return S > KT ? KT : S;
 }
 
-static int glds_split(int KT, int blocks);
-
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
+  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
   const int mtiles = (T + 15) / 16;
   if (mtiles <= 4) return 0;
   const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
   const int MTW = mtiles <= 8 ? 2 : 3;
   const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
   const int nblk = (ntiles + 7) / 8;
-  const int S = std::max(mid_split(K / 32, nblk * mblocks), glds_split(K / 32, nblk * mblocks));
+  const int S = mid_split(K / 32, nblk * mblocks);
   return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
 }
 
-// k-split for the one-workgroup-per-CU DMA kernel: whole waves of 256
-// workgroups, ~8 k-steps of pipeline fill per workgroup.
-static int glds_split(int KT, int blocks) {
-  static const int force = getenv("FFMI_GEMM_S") ? atoi(getenv("FFMI_GEMM_S")) : 0;
-  if (force > 0) return force > KT ? KT : force;
-  int best = 1;
-  long bestc = -1;
-  for (int S = 1; S <= 8 && S <= KT; ++S) {
-    const long rounds = (blocks * (long)S + 255) / 256;
-    const long c = rounds * ((KT + S - 1) / S + 8) + (S > 1 ? 4 : 0);
-    if (bestc < 0 || c < bestc) best = S, bestc = c;
-  }
-  return best;
-}
-
-static bool use_glds() {
-  static const bool v = getenv("FFMI_GEMM_IMPL") && !strcmp(getenv("FFMI_GEMM_IMPL"), "glds");
-  return v;
-}
-
-template <int MTW, int NST>
-static hipError_t run_glds(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
-                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s) {
-  constexpr int NTW = 8;
-  const int KT = K / 32;
-  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
-  const int mtiles = (T + 15) / 16;
-  const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
-  const int nblk = (ntiles + NTW - 1) / NTW;
-  int S = glds_split(KT, nblk * mblocks);
-  const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
-  if (S > 1 && (!ws || ws_bytes < need)) S = 1;
-  dim3 grid(nblk, S, mblocks);
-  if (epi)
-    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NTW, NST, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws,
-                       T, N, K, KT, ntiles, S);
-  else
-    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NTW, NST, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws,
-                       T, N, K, KT, ntiles, S);
-  if (S > 1) {
-    const long total = (long)T * N;
-    const unsigned blocks = (unsigned)((total + 255) / 256);
-    if (epi)
-      hipLaunchKernelGGL(gemm_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S);
-    else
-      hipLaunchKernelGGL(gemm_reduce_kernel<0>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S);
-  }
-  return hipGetLastError();
-}
-
-template <int MTW>
+template <int MTW, int PF>
 static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
-                          size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s) {
+                          size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s,
+                          bool xpacked, int yp) {
   constexpr int NTW = 8;
   const int KT = K / 32;
   const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
@@ -629,21 +503,33 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
   if (S > 1 && (!ws || ws_bytes < need)) S = 1;  // no workspace: un-split (slower)
   dim3 grid(nblk, S, mblocks);
-  if (epi)
-    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
-                       K, KT, ntiles, S);
+  static const bool stamp = getenv("FFMI_GEMM_STAMP") != nullptr;
+  if (xpacked) {
+    if (epi)
+      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 1, false, true>), grid, dim3(256), 0, s, X,
+                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);
+    else
+      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0, false, true>), grid, dim3(256), 0, s, X,
+                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);
+  } else if (stamp && !epi && stamp_buf()) {
+    g_stamp_entries = (long)nblk * S * mblocks * 4;
+    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0, true>), grid, dim3(256), 0, s, X, Wp, Y,
+                       ws, T, N, K, KT, ntiles, S, yp);
+  } else if (epi)
+    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
+                       K, KT, ntiles, S, yp);
   else
-    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
-                       K, KT, ntiles, S);
+    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
+                       K, KT, ntiles, S, yp);
   if (S > 1) {
-    const long total = (long)T * N;
+    const long total = (long)T * ((N + 3) / 4);
     const unsigned blocks = (unsigned)((total + 255) / 256);
     if (epi)
       hipLaunchKernelGGL(gemm_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S);
+                         ntiles, S, yp);
     else
       hipLaunchKernelGGL(gemm_reduce_kernel<0>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S);
+                         ntiles, S, yp);
   }
   return hipGetLastError();
 }
@@ -653,32 +539,48 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
   const int mtiles = (T + 15) / 16;
-  static const int mid_impl = [] {
-    const char *e = getenv("FFMI_GEMM_IMPL");
-    if (!e) return 0;
-    if (!strcmp(e, "skinny4")) return 4;
-    if (!strcmp(e, "skinny8")) return 8;
-    if (!strcmp(e, "skinny2")) return 2;
-    return 0;
-  }();
-  if (mtiles > 4 && mid_impl == 4)
-    return dispatch_nt<4, 4, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 3) / 4, s);
-  if (mtiles > 4 && mid_impl == 8)
-    return dispatch_nt<8, 2, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 7) / 8, s);
-  if (mtiles > 2 && mid_impl == 2)
-    return dispatch_nt<2, 8, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 1) / 2, s);
-  if (mtiles > 4 && use_glds()) {
-    if (mtiles > 8) return run_glds<3, 6>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
-    return run_glds<2, 7>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
-  }
-  if (mtiles > 8) return run_mid<3>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
-  if (mtiles > 4) return run_mid<2>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s);
-  if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
-  if (mtiles <= 2) return dispatch_nt<2, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
-  if (mtiles <= 4) return dispatch_nt<4, 4, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
-  if (mtiles <= 8) return dispatch_nt<8, 2, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
-  if (mtiles <= 12) return dispatch_nt<12, 2, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s);
-  return dispatch_nt<12, 2, 1>(X, Wp, Y, T, N, K, KT, epilogue, (mtiles + 11) / 12, s);
+  const bool xp = (epilogue & FFMI_X_PACKED) != 0;
+  const int yp = (epilogue & FFMI_Y_PACKED) ? 1 : 0;
+  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
+  if ((xp && K % 32) || (yp && N % 32)) return hipErrorInvalidValue;
+  if (mtiles > 8) return run_mid<3, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp);
+  if (mtiles > 4) return run_mid<2, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp);
+  const int xi = xp ? 1 : 0;
+  if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
+  if (mtiles <= 2) return dispatch_nt<2, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
+  return dispatch_nt<4, 4, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
+}
+
+// Packed activation tiles: Xp[mt][kt][lane][8] = X[mt*16 + (lane&15)][kt*32 + 8(lane>>4) + e]
+// (rows >= T zero) -- the MFMA operand fragment order of the weights (weights.hip),
+// so a GEMM reads each activation fragment as one contiguous 1 KiB.
+__global__ void pack_act_kernel(const uint16_t *__restrict__ X, uint16_t *__restrict__ Xp, int T,
+                                int K, int KT) {
+  const int mt = blockIdx.y, kt = blockIdx.x, l = threadIdx.x;
+  const int r = mt * 16 + (l & 15);
+  uint4 v = make_uint4(0, 0, 0, 0);
+  if (r < T) v = *reinterpret_cast<const uint4 *>(X + (size_t)r * K + kt * 32 + 8 * (l >> 4));
+  *reinterpret_cast<uint4 *>(Xp + (((size_t)mt * KT + kt) * 64 + l) * 8) = v;
+}
+
+size_t packed_act_bytes(int T, int K) { return (size_t)((T + 15) / 16) * 16 * K * 2; }
+
+hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  hipLaunchKernelGGL(pack_act_kernel, dim3(K / 32, (T + 15) / 16), dim3(64), 0, s, X, Xp, T, K,
+                     K / 32);
+  return hipGetLastError();
+}
+
+// diagnostics: stamps of the last FFMI_GEMM_STAMP launch (6 int64 per wave)
+long gemm_debug_stamps(long long *dst, long max_waves) {
+  long long *buf = stamp_buf();
+  const long n = g_stamp_entries < max_waves ? g_stamp_entries : max_waves;
+  if (!buf || n <= 0) return 0;
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(dst, buf, (size_t)n * 6 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
 }
 
 }  // namespace ffmi

@@ -31,7 +31,7 @@ template <int MAXC>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
-    uint16_t *__restrict__ out, int H, float eps) {
+    uint16_t *__restrict__ out, int H, float eps, int out_packed) {
   __shared__ float scratch[4];
   const int row = blockIdx.x;
   const int nchunk = H >> 3;
@@ -79,30 +79,32 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
         float y = h2f_(f2h_(__fmul_rn(h2f_(e[q]), rms)));
         o8[q] = f2h_(__fmul_rn(y, h2f_(we[q])));
       }
-      *reinterpret_cast<uint4 *>(out + (size_t)row * H + ch * 8) =
-          *reinterpret_cast<uint4 *>(o8);
+      uint16_t *dst = out_packed ? out + act_packed_off(row, ch * 8, H) : out + (size_t)row * H + ch * 8;
+      *reinterpret_cast<uint4 *>(dst) = *reinterpret_cast<uint4 *>(o8);
     }
   }
 }
 
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s) {
+                          hipStream_t s, bool out_packed) {
   if (T <= 0) return hipSuccess;
+  if (out_packed && H % 32) return hipErrorInvalidValue;
+  const int op = out_packed ? 1 : 0;
   if (H % 8 != 0 || H > 8 * 256 * 8) return hipErrorInvalidValue;
   const int nchunk = H / 8;
   if (nchunk <= 256)
     hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps);
+                       H, eps, op);
   else if (nchunk <= 512)
     hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps);
+                       H, eps, op);
   else if (nchunk <= 1024)
     hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps);
+                       H, eps, op);
   else
     hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps);
+                       H, eps, op);
   return hipGetLastError();
 }
 

@@ -35,6 +35,10 @@ struct LlamaGPU : public ffmi_model {
   ffmi_llama_config c{};
   ffmi_model_opts o{};
   int Hl = 0, Fl = 0, d = 0, heads_l = 0, slots = 0;
+  // GEMM inputs (normed hidden, attention output, SiLU output) are kept in
+  // packed activation tiles: every GEMM then reads its activation fragments
+  // as contiguous 1 KiB blocks, like the weights (see act_packed_off)
+  bool packed = false;
   hipStream_t stream = nullptr;
   std::vector<Layer> layers;
   uint16_t *embed = nullptr, *final_norm = nullptr, *lm = nullptr;
@@ -179,7 +183,8 @@ struct LlamaGPU : public ffmi_model {
     Fl = F / P;
     FFMI_CHECK(H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0, FFMI_ERR_UNSUPPORTED);
     FFMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
-    const int Tm = o.max_tokens;
+    const int Tm = (o.max_tokens + 15) & ~15;  // packed tiles cover 16-row groups
+    packed = H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0;
     ffmi_status st;
 #define TRY(x) \
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
@@ -193,12 +198,16 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&logits, (size_t)Tm * V));
     TRY(alloc(&ids_d, (size_t)Tm * 4));
     {
-      const size_t w1 = ffmi_linear_workspace_bytes(Tm, 3 * Hl, H, FFMI_EPI_NONE);
-      const size_t w2 = ffmi_linear_workspace_bytes(Tm, H, Hl, FFMI_EPI_NONE);
-      const size_t w3 = ffmi_linear_workspace_bytes(Tm, Fl, H, FFMI_EPI_SILU_MUL);
-      const size_t w4 = ffmi_linear_workspace_bytes(Tm, H, Fl, FFMI_EPI_NONE);
-      const size_t w5 = ffmi_linear_workspace_bytes(Tm, V, H, FFMI_EPI_NONE);
-      ws_bytes = std::max(std::max(std::max(w1, w2), std::max(w3, w4)), w5);
+      // the split-K factor depends on the row-block count, so take the max
+      // over every batch size the model can see
+      for (int t = 16; t <= Tm; t += 16) {
+        const size_t w1 = ffmi_linear_workspace_bytes(t, 3 * Hl, H, FFMI_EPI_NONE);
+        const size_t w2 = ffmi_linear_workspace_bytes(t, H, Hl, FFMI_EPI_NONE);
+        const size_t w3 = ffmi_linear_workspace_bytes(t, Fl, H, FFMI_EPI_SILU_MUL);
+        const size_t w4 = ffmi_linear_workspace_bytes(t, H, Fl, FFMI_EPI_NONE);
+        const size_t w5 = ffmi_linear_workspace_bytes(t, V, H, FFMI_EPI_NONE);
+        ws_bytes = std::max(ws_bytes, std::max(std::max(std::max(w1, w2), std::max(w3, w4)), w5));
+      }
       if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
     }
     TRY(alloc(&probs_d, (size_t)Tm * 4));
@@ -263,6 +272,7 @@ struct LlamaGPU : public ffmi_model {
       ac.max_tokens = Tm;
       ac.qk_scale = 1.0f / sqrtf((float)d);
       ac.rope_theta = c.rope_theta;
+      ac.out_layout = packed ? 1 : 0;
       TRY(ffmi_attn_create(&ac, &L.attn));
       int sl = 0;
       ffmi_attn_kv_ptrs(L.attn, nullptr, nullptr, &sl);
@@ -306,13 +316,11 @@ struct LlamaGPU : public ffmi_model {
       Layer &L = layers[l];
       const bool on = prof_on(l, T);
       pr = prof_begin(on);
-      if (l == 0)
-        TRY(ffmi_rmsnorm(res, L.in_norm, h, T, H, eps, s));
-      else
-        TRY(ffmi_residual_rmsnorm(res, proj, L.in_norm, res, h, T, H, eps, s));
+      const int XP = packed ? FFMI_X_PACKED : 0, YP = packed ? FFMI_Y_PACKED : 0;
+      TRY(ffmi_rmsnorm_ex(res, l == 0 ? nullptr : proj, L.in_norm, res, h, T, H, eps, YP, s));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 2 : 4), 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE, ws, ws_bytes, s));
+      TRY(ffmi_linear_ws(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
       pr = prof_begin(on);
       if (mode == FFMI_MODEL_TREE)
@@ -323,29 +331,30 @@ struct LlamaGPU : public ffmi_model {
         TRY(ffmi_attn_inc(L.attn, batch, qkv, att, s));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE, ws, ws_bytes, s));
+      TRY(ffmi_linear_ws(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
       prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
       prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
       pr = prof_begin(on);
-      TRY(ffmi_residual_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, s));
+      TRY(ffmi_rmsnorm_ex(res, proj, L.post_norm, res, h, T, H, eps, YP, s));
       prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL, ws, ws_bytes, s));
+      TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE, ws, ws_bytes, s));
+      TRY(ffmi_linear_ws(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
       prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
       prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
     }
+    const int XP = packed ? FFMI_X_PACKED : 0, YP = packed ? FFMI_Y_PACKED : 0;
     pr = prof_begin(ptail);
-    TRY(ffmi_residual_rmsnorm(res, proj, final_norm, res, h, T, H, eps, s));
+    TRY(ffmi_rmsnorm_ex(res, proj, final_norm, res, h, T, H, eps, YP, s));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
     pr = prof_begin(ptail);
-    TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE, ws, ws_bytes, s));
+    TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
     pr = prof_begin(ptail);
     if (k == 1)

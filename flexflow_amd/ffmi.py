@@ -19,6 +19,8 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "hip error", 3: "rccl error", 4: "o
 ATTN_INC, ATTN_SPEC, ATTN_TREE = 0, 1, 2
 MODEL_INC, MODEL_BEAM, MODEL_TREE = 0, 1, 2
 EPI_NONE, EPI_SILU_MUL = 0, 1
+X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
+Y_PACKED = 0x20  # FFMI_Y_PACKED
 F16, F32, I32 = 0, 1, 2
 ATTN_QTILE = 16
 MAX_TREE = 64
@@ -49,7 +51,8 @@ class BatchDesc(ctypes.Structure):
 class AttnCfg(ctypes.Structure):
     _fields_ = [("mode", c_int), ("num_heads", c_int), ("head_dim", c_int),
                 ("max_requests", c_int), ("max_seq_len", c_int), ("max_tree_tokens", c_int),
-                ("max_tokens", c_int), ("qk_scale", c_float), ("rope_theta", c_float)]
+                ("max_tokens", c_int), ("qk_scale", c_float), ("rope_theta", c_float),
+                ("out_layout", c_int)]
 
 
 class LlamaConfig(ctypes.Structure):
@@ -147,6 +150,11 @@ SIGNATURES = {
     "ffmi_status_str": (ctypes.c_char_p, [c_int]),
     "ffmi_version": (ctypes.c_char_p, []),
     "ffmi_last_error": (ctypes.c_char_p, []),
+    "ffmi_packed_activation_bytes": (ctypes.c_size_t, [c_int, c_int]),
+    "ffmi_rmsnorm_ex": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int,
+                                c_float, c_int, c_void_p]),
+    "ffmi_pack_activations": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "ffmi_debug_gemm_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
 }
 
 _lib = None

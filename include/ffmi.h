@@ -118,6 +118,9 @@ typedef struct {
   int max_tokens;      /* batch capacity (staging rows for TREE commits)     */
   float qk_scale;      /* 1/sqrt(head_dim) (qk_prod_scaling)                 */
   float rope_theta;    /* HF rotate-half RoPE base                           */
+  int out_layout;      /* 0: out [T][heads*head_dim] row-major;
+                          1: packed activation tiles (feeds ffmi_linear with
+                          FFMI_X_PACKED; heads*head_dim % 32 == 0)          */
 } ffmi_attn_cfg;
 
 typedef struct ffmi_attn ffmi_attn;
@@ -149,6 +152,17 @@ typedef enum {
                            (fuses SigmoidSiluMulti, sigmoid_silu_multi.cu:37-47) */
 } ffmi_epilogue;
 
+/* OR into `epilogue`: X is in packed activation tiles (ffmi_pack_activations)
+ * instead of row-major [T][K] -- the operand-fragment order of the weights, so
+ * a GEMM reads each activation fragment as one contiguous 1 KiB.  T > 64. */
+#define FFMI_X_PACKED 0x10
+/* OR into `epilogue`: write Y in packed activation tiles (a GEMM input of the
+ * next layer; out_dim % 32 == 0). */
+#define FFMI_Y_PACKED 0x20
+size_t ffmi_packed_activation_bytes(int T, int in_dim);
+ffmi_status ffmi_pack_activations(const void *X, int T, int in_dim, void *X_packed,
+                                  ffmi_stream stream);
+
 /* Bytes of the MFMA-swizzled weight for an [N][K] fp16 matrix. */
 size_t ffmi_linear_packed_bytes(int out_dim, int in_dim);
 /* [N][K] row-major fp16 (HF layout) -> MFMA fragment order.  For
@@ -177,6 +191,10 @@ ffmi_status ffmi_rmsnorm(const void *x, const void *w, void *out, int T, int H,
 ffmi_status ffmi_residual_rmsnorm(const void *x1, const void *x2, const void *w,
                                   void *residual_out, void *out, int T, int H,
                                   float eps, ffmi_stream stream);
+/* Either norm (x2 == NULL: plain RMSNorm) with flags: FFMI_Y_PACKED writes
+ * `out` in packed activation tiles for a following ffmi_linear. */
+ffmi_status ffmi_rmsnorm_ex(const void *x1, const void *x2, const void *w, void *residual_out,
+                            void *out, int T, int H, float eps, int flags, ffmi_stream stream);
 
 /* ------------------------------------------------------------------------ */
 /* Tensor-parallel all-reduce (replaces Kernels::AllReduce::                 */
@@ -305,6 +323,12 @@ ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
                                         int max_seq, int max_tree, uint64_t salt,
                                         int disagree_pct, ffmi_model **out);
+
+/* Diagnostics: with FFMI_GEMM_STAMP set in the environment, M-split GEMM
+ * launches record per-wave timestamps; copies the last launch's records
+ * ({start, prologue done, k-loop done, end} at 100 MHz, HW_ID, XCC_ID) and
+ * returns the number of waves (<= max_waves). */
+long ffmi_debug_gemm_stamps(long long *dst, long max_waves);
 
 const char *ffmi_status_str(ffmi_status s);
 /* message + file:line of the last failing check on this process */

@@ -29,6 +29,8 @@ def main():
     ap.add_argument("--shapes", default="llama7b")
     ap.add_argument("--T", default="1,8,24,64,168,192")
     ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--xpacked", action="store_true", help="pre-pack X (FFMI_X_PACKED)")
+    ap.add_argument("--ops", default="", help="comma list of op names to run (default all)")
     ap.add_argument("--cold-mb", type=int, default=768,
                     help="rotate weight copies totalling this many MB (0: one hot copy)")
     args = ap.parse_args()
@@ -36,6 +38,8 @@ def main():
     rng = np.random.default_rng(0)
     res = []
     for name, N, K, epi in SHAPES[args.shapes]:
+        if args.ops and name not in args.ops.split(","):
+            continue
         rows = 2 * N if epi else N
         W = f16(rng.uniform(-0.05, 0.05, (rows, K)))
         nb = L.ffmi_linear_packed_bytes(rows, K)
@@ -57,14 +61,23 @@ def main():
             Wps.append(c)
         for T in [int(t) for t in args.T.split(",")]:
             Xs = [Buf(f16(rng.standard_normal((T, K)))) for _ in range(len(Wps))]
+            flag = 0
+            if args.xpacked and T > 64:
+                flag = F.X_PACKED
+                packed = []
+                for xb in Xs:
+                    xp = Buf.empty((L.ffmi_packed_activation_bytes(T, K) // 2,), np.uint16)
+                    F.check(L.ffmi_pack_activations(xb.ptr, T, K, xp.ptr, None))
+                    packed.append(xp)
+                Xs = packed
             Y = Buf.empty((T, N), np.float16)
             for i in range(len(Wps)):
-                F.check(L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi, None))
+                F.check(L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None))
             tm = Timer()
             tm.start()
             for it in range(args.iters):
                 i = it % len(Wps)
-                L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi, None)
+                L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None)
             ms = tm.stop() / args.iters
             byts = 2.0 * (rows * K + T * K + T * N)
             r = dict(op=name, T=T, N=N, K=K, copies=len(Wps), us=round(ms * 1e3, 2),

@@ -39,6 +39,6 @@ def test_invalid_arguments_return_status_not_abort():
     L = F.lib()
     assert L.ffmi_linear(None, None, None, 1, 16, 32, 0, None) == 1
     assert L.ffmi_rmsnorm(None, None, None, 1, 8, 1e-6, None) == 1
-    cfg = F.AttnCfg(0, 2, 96, 1, 16, 0, 16, 0.1, 10000.0)  # head_dim 96 unsupported
+    cfg = F.AttnCfg(0, 2, 96, 1, 16, 0, 16, 0.1, 10000.0, 0)  # head_dim 96 unsupported
     h = ctypes.c_void_p()
     assert L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(h)) == 5

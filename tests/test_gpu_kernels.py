@@ -74,6 +74,82 @@ def test_linear_matches_oracle(T, N, K):
     close16(Yb.get(), ref)
 
 
+@pytest.mark.parametrize("T", [65, 100, 168, 200])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_linear_packed_activations_bit_identical(T, epi):
+    """FFMI_X_PACKED (activation fragment tiles) changes only the load layout:
+    the result must be bit-identical to the row-major input."""
+    rng = np.random.default_rng(T + epi)
+    N, K = 704, 1024
+    X = f16(rng.standard_normal((T, K)))
+    if epi:
+        Wg, Wu = f16(rng.uniform(-0.05, 0.05, (N, K))), f16(rng.uniform(-0.05, 0.05, (N, K)))
+        gb, ub = Buf(Wg), Buf(Wu)
+        Wp = Buf.empty((2 * L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+    else:
+        Wp = packed(f16(rng.uniform(-0.05, 0.05, (N, K))))
+    Xb = Buf(X)
+    Xp = Buf.empty((L.ffmi_packed_activation_bytes(T, K) // 2,), np.uint16)
+    F.check(L.ffmi_pack_activations(Xb.ptr, T, K, Xp.ptr, None))
+    Y0, Y1 = Buf.empty((T, N), np.float16), Buf.empty((T, N), np.float16)
+    F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y0.ptr, T, N, K, epi, None))
+    F.check(L.ffmi_linear(Xp.ptr, Wp.ptr, Y1.ptr, T, N, K, epi | F.X_PACKED, None))
+    assert np.array_equal(Y0.get().view(np.uint16), Y1.get().view(np.uint16))
+
+
+def test_pack_activations_matches_numpy_twin():
+    rng = np.random.default_rng(3)
+    T, K = 37, 256
+    X = f16(rng.standard_normal((T, K)))
+    Xb = Buf(X)
+    Xp = Buf.empty((L.ffmi_packed_activation_bytes(T, K) // 2,), np.uint16)
+    F.check(L.ffmi_pack_activations(Xb.ptr, T, K, Xp.ptr, None))
+    assert np.array_equal(Xp.get(), pack_act_np(X).view(np.uint16))
+
+
+@pytest.mark.parametrize("T", [1, 8, 40, 64, 100, 168])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_linear_packed_in_and_out_bit_identical(T, epi):
+    """Skinny and M-split paths with X_PACKED | Y_PACKED == row-major, bit for bit."""
+    rng = np.random.default_rng(1000 + T + epi)
+    N, K = 704, 512
+    X = f16(rng.standard_normal((T, K)))
+    if epi:
+        Wg, Wu = f16(rng.uniform(-0.05, 0.05, (N, K))), f16(rng.uniform(-0.05, 0.05, (N, K)))
+        gb, ub = Buf(Wg), Buf(Wu)
+        Wp = Buf.empty((2 * L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+    else:
+        Wp = packed(f16(rng.uniform(-0.05, 0.05, (N, K))))
+    Xb = Buf(X)
+    Xp = Buf(pack_act_np(X))
+    Tp = (T + 15) // 16 * 16
+    Y0, Y1 = Buf.empty((T, N), np.float16), Buf.empty((Tp, N), np.float16)
+    F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y0.ptr, T, N, K, epi, None))
+    F.check(L.ffmi_linear(Xp.ptr, Wp.ptr, Y1.ptr, T, N, K, epi | F.X_PACKED | F.Y_PACKED, None))
+    y1 = unpack_act_np(Y1.get().reshape(-1), T, N)
+    assert np.array_equal(Y0.get().view(np.uint16), y1.view(np.uint16))
+
+
+@pytest.mark.parametrize("resid", [0, 1])
+def test_rmsnorm_packed_output(resid):
+    rng = np.random.default_rng(5 + resid)
+    T, H = 21, 4096
+    x1, x2 = f16(rng.standard_normal((T, H))), f16(rng.standard_normal((T, H)))
+    w = f16(1 + 0.1 * rng.standard_normal(H))
+    a, b, wb = Buf(x1), Buf(x2), Buf(w)
+    r0, o0 = Buf.empty((T, H), np.float16), Buf.empty((T, H), np.float16)
+    r1, o1 = Buf.empty((T, H), np.float16), Buf.empty((32, H), np.float16)
+    x2p = b.ptr if resid else None
+    F.check(L.ffmi_rmsnorm_ex(a.ptr, x2p, wb.ptr, r0.ptr, o0.ptr, T, H, 1e-6, 0, None))
+    F.check(L.ffmi_rmsnorm_ex(a.ptr, x2p, wb.ptr, r1.ptr, o1.ptr, T, H, 1e-6, F.Y_PACKED, None))
+    assert np.array_equal(unpack_act_np(o1.get().reshape(-1), T, H).view(np.uint16),
+                          o0.get().view(np.uint16))
+    if resid:
+        assert np.array_equal(r0.get().view(np.uint16), r1.get().view(np.uint16))
+
+
 @pytest.mark.parametrize("T", [1, 8, 24, 168])
 def test_linear_gate_up_silu_fused(T):
     rng = np.random.default_rng(T)
@@ -138,7 +214,7 @@ def test_softmax_argmax_topk_exact(V):
     T = 9
     logits = f16(rng.standard_normal((T, V)) * 2)
     # planted exact ties and near-ties that fp16 softmax collapses
-    logits[1, 17] = logits[1, 900] = f16(9.0)
+    logits[1, 17] = logits[1, V - 100] = f16(9.0)
     logits[2, 5] = f16(8.0)
     logits[2, 6] = f16(8.0 + 2 ** -7)
     lb = Buf(logits)
@@ -156,14 +232,30 @@ def test_softmax_argmax_topk_exact(V):
 
 
 # ---------------------------------------------------------------- attention
+def pack_act_np(X):
+    """numpy twin of ffmi_pack_activations: [T][K] -> [T/16][K/32][64 lanes][8]."""
+    T, K = X.shape
+    Tp = (T + 15) // 16 * 16
+    Xp = np.zeros((Tp, K), X.dtype)
+    Xp[:T] = X
+    return Xp.reshape(Tp // 16, 16, K // 32, 4, 8).transpose(0, 2, 3, 1, 4).reshape(-1)
+
+
+def unpack_act_np(P, T, K):
+    Tp = (T + 15) // 16 * 16
+    return P[:Tp * K].reshape(Tp // 16, K // 32, 4, 16, 8).transpose(0, 3, 1, 2, 4).reshape(Tp, K)[:T]
+
+
 class AttnCase:
     """Builds token-info batches for ffmi_attn_* and the matching oracle."""
 
-    def __init__(self, mode, heads=2, d=128, max_requests=4, max_seq=96, tree=32, max_tokens=128):
+    def __init__(self, mode, heads=2, d=128, max_requests=4, max_seq=96, tree=32, max_tokens=128,
+                 out_layout=0):
         self.heads, self.d = heads, d
         self.Hl = heads * d
+        self.out_layout = out_layout
         cfg = F.AttnCfg(mode, heads, d, max_requests, max_seq, tree, max_tokens,
-                        1.0 / np.sqrt(d), 10000.0)
+                        1.0 / np.sqrt(d), 10000.0, out_layout)
         self.h = ctypes.c_void_p()
         F.check(L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(self.h)))
         self.b = ctypes.c_void_p()
@@ -210,11 +302,13 @@ class AttnCase:
             mk = (ctypes.c_uint64 * flat.size)(*flat.ravel().tolist())
         desc = F.BatchDesc(T, len(work), len(commits), nmask, toks, wk, cm, mk)
         F.check(L.ffmi_batch_upload(self.b, ctypes.byref(desc), None))
-        qb, ob = Buf(qkv), Buf.empty((T, self.Hl), np.float16)
+        Tp = (T + 15) // 16 * 16
+        qb, ob = Buf(qkv), Buf.empty((Tp, self.Hl), np.float16)
         fn = {F.ATTN_INC: L.ffmi_attn_inc, F.ATTN_SPEC: L.ffmi_attn_spec,
               F.ATTN_TREE: L.ffmi_attn_tree}[self.mode]
         F.check(fn(self.h, self.b, qb.ptr, ob.ptr, None))
         out = ob.get()
+        out = unpack_act_np(out.reshape(-1), T, self.Hl) if self.out_layout else out[:T]
         # oracle side: commits, stores, then attention rows
         if commits:
             for (src, req, depth) in commits:
@@ -242,10 +336,11 @@ class AttnCase:
         return ref.reshape(-1)
 
 
+@pytest.mark.parametrize("layout", [0, 1])
 @pytest.mark.parametrize("d", [64, 128])
-def test_attention_inc_prefill_then_decode(d):
+def test_attention_inc_prefill_then_decode(d, layout):
     rng = np.random.default_rng(d)
-    c = AttnCase(F.ATTN_INC, d=d)
+    c = AttnCase(F.ATTN_INC, d=d, out_layout=layout)
     # step 1: prefill of three requests (chunked positions), step 2: decode/chunk
     lens = {0: 20, 1: 37, 2: 10}
     infos = [(5, p, r, p, p + 1, 0, 0, 0) for r, n in lens.items() for p in range(n)]
