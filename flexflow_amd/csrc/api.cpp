@@ -212,10 +212,12 @@ extern "C" ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *
   return FFMI_OK;
 }
 
-static ffmi_status attn_run(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, void *out,
-                            ffmi_stream stream, bool tree) {
-  FFMI_CHECK(h && b && qkv && out, FFMI_ERR_INVALID);
+namespace ffmi {
+ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
+                         void *out, ffmi_stream stream) {
+  FFMI_CHECK(h && b && (qkv || qkvp.S > 0) && out, FFMI_ERR_INVALID);
   FFMI_CHECK(b->num_tokens <= h->cfg.max_tokens, FFMI_ERR_INVALID);
+  const bool tree = h->cfg.mode == FFMI_ATTN_TREE;
   const hipStream_t s = (hipStream_t)stream;
   const int heads = h->cfg.num_heads, d = h->cfg.head_dim;
   if (tree && b->num_commits > 0)
@@ -223,25 +225,33 @@ static ffmi_status attn_run(ffmi_attn *h, const ffmi_batch_dev *b, const void *q
                                  h->slots, s));
   FFMI_HIP(ffmi::launch_rope_store(b->dev, b->num_tokens, (const uint16_t *)qkv, h->qbuf, h->kc,
                                    h->vc, tree ? h->stage : nullptr, h->rope, heads, d, h->slots,
-                                   h->slots, s));
+                                   h->slots, s, qkvp));
   FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, h->qbuf, h->kc, h->vc, (uint16_t *)out,
                                   heads, d, h->slots, h->cfg.qk_scale, s,
                                   h->cfg.out_layout == 1));
   return FFMI_OK;
 }
+}  // namespace ffmi
+
+static ffmi_status attn_run(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, void *out,
+                            ffmi_stream stream, int mode) {
+  FFMI_CHECK(h && qkv, FFMI_ERR_INVALID);
+  FFMI_CHECK(h->cfg.mode == mode, FFMI_ERR_INVALID);  // handle made for this op
+  return ffmi::attn_forward(h, b, qkv, ffmi::Partials(), out, stream);
+}
 
 extern "C" ffmi_status ffmi_attn_inc(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
                                      void *out, ffmi_stream stream) {
-  return attn_run(h, b, qkv, out, stream, false);
+  return attn_run(h, b, qkv, out, stream, FFMI_ATTN_INC);
 }
 extern "C" ffmi_status ffmi_attn_spec(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
                                       void *out, ffmi_stream stream) {
-  return attn_run(h, b, qkv, out, stream, false);
+  return attn_run(h, b, qkv, out, stream, FFMI_ATTN_SPEC);
 }
 extern "C" ffmi_status ffmi_attn_tree(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
                                       void *out, ffmi_stream stream) {
   FFMI_CHECK(h && h->stage, FFMI_ERR_INVALID);  // created with FFMI_ATTN_TREE
-  return attn_run(h, b, qkv, out, stream, true);
+  return attn_run(h, b, qkv, out, stream, FFMI_ATTN_TREE);
 }
 
 // ---------------------------------------------------------------------------

@@ -66,21 +66,41 @@ __device__ __forceinline__ BatchView batch_view(const char *blob) {
   return v;
 }
 
+// Split-K partial sums left in the GEMM workspace for the CONSUMER to combine
+// (S fp32 slabs [S][T][NP]; value(t, n) = fp16(sum over s in order)), which
+// saves the separate reduce pass.  S == 0: nothing deferred, read Y.
+struct Partials {
+  const float *p = nullptr;
+  int S = 0, NP = 0;
+};
+__device__ __forceinline__ float partials_value(const float *p, int S, int NP, int T, int t,
+                                                int n) {
+  const size_t slab = (size_t)T * NP;
+  const float *q = p + (size_t)t * NP + n;
+  float acc = q[0];
+  for (int s = 1; s < S; ++s) acc += q[s * slab];
+  return __half2float(__float2half_rn(acc));
+}
+
 // ---- kernel launchers (defined in kernels/*.hip) ----
 hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
                               hipStream_t s);
 hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
                               int N, int K, uint16_t *dst, int interleave_gate_up,
                               int tile_offset, hipStream_t s);
+// defer != nullptr: a split-K plan skips its reduce pass and describes the
+// slabs in *defer (the caller's next kernel combines them); otherwise / S == 1
+// Y is written and defer->S = 0.  Only for FFMI_EPI_NONE.
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
-                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s);
+                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
+                       Partials *defer = nullptr);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
 long gemm_debug_stamps(long long *dst, long max_waves);
 size_t packed_act_bytes(int T, int K);
 hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s);
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s, bool out_packed = false);
+                          hipStream_t s, bool out_packed = false, Partials x2p = {});
 hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
                             uint16_t *out, int H, hipStream_t s);
 hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
@@ -90,7 +110,7 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
 hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv,
                              uint16_t *qbuf, uint16_t *kc, uint16_t *vc,
                              uint16_t *stage, const float *rope, int heads, int d,
-                             int slots, int max_rope_pos, hipStream_t s);
+                             int slots, int max_rope_pos, hipStream_t s, Partials qkvp = {});
 hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
                          uint16_t *kc, uint16_t *vc, int heads, int d, int slots,
                          hipStream_t s);
@@ -113,3 +133,10 @@ struct ffmi_batch_dev {
   int num_tokens = 0, num_work = 0, num_commits = 0, num_mask_reqs = 0;
   hipEvent_t uploaded = nullptr;  // guards reuse of the pinned staging
 };
+
+// Internal entry points used by the in-library model runtime (llama_gpu.cpp):
+// the public ffmi_attn_* / ffmi_rmsnorm_ex with deferred split-K inputs.
+namespace ffmi {
+ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
+                         void *out, ffmi_stream stream);
+}  // namespace ffmi

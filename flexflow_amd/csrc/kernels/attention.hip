@@ -47,7 +47,8 @@ __global__ void rope_store_kernel(const char *__restrict__ blob, int T,
                                   uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
                                   uint16_t *__restrict__ vc, uint16_t *__restrict__ stage,
                                   const float *__restrict__ rope, int heads, int d,
-                                  int slots, int max_rope_pos) {
+                                  int slots, int max_rope_pos, const float *__restrict__ part,
+                                  int pS, int pNP) {
   const int hd = d >> 1;
   const int ppb = blockDim.x / hd;
   const int pair = blockIdx.x * ppb + threadIdx.x / hd;
@@ -57,20 +58,24 @@ __global__ void rope_store_kernel(const char *__restrict__ blob, int T,
   BatchView bv = batch_view(blob);
   const ffmi_token_info ti = bv.tokens[t];
   const int Hl = heads * d;
-  const uint16_t *qrow = qkv + (size_t)t * 3 * Hl + h * d;
-  const uint16_t *krow = qrow + Hl;
-  const uint16_t *vrow = qrow + 2 * Hl;
+  // qkv element of this token: the fp16 GEMM output, or the in-order sum of
+  // its deferred split-K slabs rounded to fp16 (the same value)
+  auto qkv_at = [&](int col) -> float {
+    return part ? partials_value(part, pS, pNP, T, t, col)
+                : h2f(qkv[(size_t)t * 3 * Hl + col]);
+  };
+  const int qc = h * d, kc0 = Hl + h * d, vc0 = 2 * Hl + h * d;
   const int pos = min(max(ti.pos, 0), max_rope_pos - 1);
   const float c = rope[((size_t)pos * hd + i) * 2 + 0];
   const float s = rope[((size_t)pos * hd + i) * 2 + 1];
-  float a = h2f(qrow[i]), b = h2f(qrow[i + hd]);
+  float a = qkv_at(qc + i), b = qkv_at(qc + i + hd);
   const uint16_t q0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
   const uint16_t q1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
-  a = h2f(krow[i]);
-  b = h2f(krow[i + hd]);
+  a = qkv_at(kc0 + i);
+  b = qkv_at(kc0 + i + hd);
   const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
   const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
-  const uint16_t v0 = vrow[i], v1 = vrow[i + hd];
+  const uint16_t v0 = f2h(qkv_at(vc0 + i)), v1 = f2h(qkv_at(vc0 + i + hd));
   uint16_t *qo = qbuf + (size_t)t * Hl + h * d;
   qo[i] = q0;
   qo[i + hd] = q1;
@@ -93,13 +98,15 @@ __global__ void rope_store_kernel(const char *__restrict__ blob, int T,
 
 hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv, uint16_t *qbuf,
                              uint16_t *kc, uint16_t *vc, uint16_t *stage, const float *rope,
-                             int heads, int d, int slots, int max_rope_pos, hipStream_t s) {
+                             int heads, int d, int slots, int max_rope_pos, hipStream_t s,
+                             Partials qkvp) {
   if (T <= 0) return hipSuccess;
   const int hd = d / 2;
   const int ppb = 256 / hd;
   const int pairs = T * heads;
   hipLaunchKernelGGL(rope_store_kernel, dim3((pairs + ppb - 1) / ppb), dim3(ppb * hd), 0, s,
-                     blob, T, qkv, qbuf, kc, vc, stage, rope, heads, d, slots, max_rope_pos);
+                     blob, T, qkv, qbuf, kc, vc, stage, rope, heads, d, slots, max_rope_pos,
+                     qkvp.S > 0 ? qkvp.p : nullptr, qkvp.S, qkvp.NP);
   return hipGetLastError();
 }
 

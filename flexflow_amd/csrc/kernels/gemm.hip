@@ -303,7 +303,7 @@ __device__ long long *g_gemm_stamps;
 __device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 
 template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false>
-__global__ __launch_bounds__(256, 2) void gemm_mid_kernel(
+__global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
     int NTILES, int S, int yp) {
@@ -471,10 +471,44 @@ __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__
   }
 }
 
-static int mid_split(int KT, int blocks) {
-  int S = (256 + blocks - 1) / blocks;
-  S = S < 1 ? 1 : (S > 8 ? 8 : S);
-  return S > KT ? KT : S;
+// Launch plan of the M-split kernel: weight tiles per workgroup (NTW) and
+// split-K factor (S).  Each workgroup is bound by its CU's load path (per-wave
+// timeline, scripts/diag_stamps.py: a k-step moves NTW KiB of weights + 4*MTW
+// KiB of activations at ~50 GB/s per CU; two workgroups on one CU each run at
+// half speed), so the plan keeps the grid within one wave of 256 workgroups,
+// prefers wide tiles (fewer activation bytes per weight byte) and charges the
+// split-K reduce pass.  Times in us; only the ranking matters.
+struct MidPlan {
+  int MTW, NTW, S, mblocks, nblk;
+};
+static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
+  MidPlan p;
+  const int mtiles = (T + 15) / 16;
+  p.MTW = mtiles <= 8 ? 2 : 3;
+  p.mblocks = (mtiles + 4 * p.MTW - 1) / (4 * p.MTW);
+  const int KT = K / 32;
+  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
+  double best = 1e30;
+  p.NTW = 8, p.S = 1;
+  // measured k-step times (us) at MTW = 3, packed activations (diag_stamps.py)
+  static const int ntw_opts[3] = {8, 12, 16};
+  static const double base[3] = {0.40, 0.65, 0.90};
+  for (int o = 0; o < 3; ++o) {
+    const int ntw = ntw_opts[o];
+    const int nblk = (ntiles + ntw - 1) / ntw;
+    for (int S = 1; S <= 8 && S <= KT; ++S) {
+      const long wgs = (long)nblk * S * p.mblocks;
+      const double rounds = (double)((wgs + 255) / 256);
+      const double steps = (double)((KT + S - 1) / S);
+      const double tstep = base[o] * (ntw + 4.0 * p.MTW) / (ntw + 12.0);
+      double t = rounds * (steps * tstep + 4.0);
+      const double slab_mb = (double)S * T * ntiles * 16 * 4 / 1e6;
+      if (S > 1) t += deferred ? slab_mb / 6.0 : 3.0 + slab_mb / 3.0;
+      if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
+    }
+  }
+  p.nblk = (ntiles + p.NTW - 1) / p.NTW;
+  return p;
 }
 
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
@@ -482,45 +516,46 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   const int mtiles = (T + 15) / 16;
   if (mtiles <= 4) return 0;
   const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
-  const int MTW = mtiles <= 8 ? 2 : 3;
-  const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
-  const int nblk = (ntiles + 7) / 8;
-  const int S = mid_split(K / 32, nblk * mblocks);
+  const int S = std::max(mid_plan(T, N, K, epilogue, false).S,
+                         epilogue ? 1 : mid_plan(T, N, K, epilogue, true).S);
   return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
 }
 
-template <int MTW, int PF>
+template <int MTW, int NTW, int PF>
 static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s,
-                          bool xpacked, int yp) {
-  constexpr int NTW = 8;
+                          bool xpacked, int yp, int S, Partials *defer) {
   const int KT = K / 32;
   const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
   const int mtiles = (T + 15) / 16;
   const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
   const int nblk = (ntiles + NTW - 1) / NTW;
-  int S = mid_split(KT, nblk * mblocks);
   const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
   if (S > 1 && (!ws || ws_bytes < need)) S = 1;  // no workspace: un-split (slower)
   dim3 grid(nblk, S, mblocks);
   static const bool stamp = getenv("FFMI_GEMM_STAMP") != nullptr;
-  if (xpacked) {
-    if (epi)
-      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 1, false, true>), grid, dim3(256), 0, s, X,
-                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);
-    else
-      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0, false, true>), grid, dim3(256), 0, s, X,
-                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);
-  } else if (stamp && !epi && stamp_buf()) {
+#define FFMI_MID(E, ST, XPK)                                                                  \
+  hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK>), grid, dim3(256), 0, s, X, Wp, \
+                     Y, ws, T, N, K, KT, ntiles, S, yp)
+  if (stamp && !epi && stamp_buf()) {
     g_stamp_entries = (long)nblk * S * mblocks * 4;
-    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0, true>), grid, dim3(256), 0, s, X, Wp, Y,
-                       ws, T, N, K, KT, ntiles, S, yp);
-  } else if (epi)
-    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 1>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
-                       K, KT, ntiles, S, yp);
-  else
-    hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, 0>), grid, dim3(256), 0, s, X, Wp, Y, ws, T, N,
-                       K, KT, ntiles, S, yp);
+    if (xpacked) FFMI_MID(0, true, true);
+    else FFMI_MID(0, true, false);
+  } else if (xpacked) {
+    if (epi) FFMI_MID(1, false, true);
+    else FFMI_MID(0, false, true);
+  } else {
+    if (epi) FFMI_MID(1, false, false);
+    else FFMI_MID(0, false, false);
+  }
+#undef FFMI_MID
+  if (defer) {
+    defer->S = 0;
+    if (S > 1 && !epi) {  // the consumer combines the slabs
+      defer->p = ws, defer->S = S, defer->NP = ntiles * 16;
+      return hipGetLastError();
+    }
+  }
   if (S > 1) {
     const long total = (long)T * ((N + 3) / 4);
     const unsigned blocks = (unsigned)((total + 255) / 256);
@@ -535,7 +570,9 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
 }
 
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
-                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s) {
+                       size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
+                       Partials *defer) {
+  if (defer) defer->S = 0;
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
   const int mtiles = (T + 15) / 16;
@@ -543,8 +580,20 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   const int yp = (epilogue & FFMI_Y_PACKED) ? 1 : 0;
   epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
   if ((xp && K % 32) || (yp && N % 32)) return hipErrorInvalidValue;
-  if (mtiles > 8) return run_mid<3, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp);
-  if (mtiles > 4) return run_mid<2, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp);
+  if (mtiles > 4) {
+    const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);
+#define FFMI_RUN(M, NW) \
+  return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer)
+    if (p.MTW == 3) {
+      if (p.NTW == 16) FFMI_RUN(3, 16);
+      if (p.NTW == 12) FFMI_RUN(3, 12);
+      FFMI_RUN(3, 8);
+    }
+    if (p.NTW == 16) FFMI_RUN(2, 16);
+    if (p.NTW == 12) FFMI_RUN(2, 12);
+    FFMI_RUN(2, 8);
+#undef FFMI_RUN
+  }
   const int xi = xp ? 1 : 0;
   if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
   if (mtiles <= 2) return dispatch_nt<2, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);

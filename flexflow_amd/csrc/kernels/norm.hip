@@ -31,9 +31,11 @@ template <int MAXC>
 __global__ __launch_bounds__(256) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
-    uint16_t *__restrict__ out, int H, float eps, int out_packed) {
+    uint16_t *__restrict__ out, int H, float eps, int out_packed,
+    const float *__restrict__ x2p, int pS, int pNP) {
   __shared__ float scratch[4];
   const int row = blockIdx.x;
+  const int T = gridDim.x;
   const int nchunk = H >> 3;
   const uint16_t *a = x1 + (size_t)row * H;
   const uint16_t *b = x2 ? x2 + (size_t)row * H : nullptr;
@@ -44,8 +46,25 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
     const int ch = threadIdx.x + c * 256;
     if (ch < nchunk) {
       uint4 xa = *reinterpret_cast<const uint4 *>(a + ch * 8);
-      if (b) {
-        uint4 xb = *reinterpret_cast<const uint4 *>(b + ch * 8);
+      if (b || x2p) {
+        uint4 xb;
+        if (x2p) {  // x2 = deferred split-K slabs of the producing GEMM, summed in order
+          const float *q = x2p + (size_t)row * pNP + ch * 8;
+          f4 lo = *reinterpret_cast<const f4 *>(q), hi = *reinterpret_cast<const f4 *>(q + 4);
+          for (int sl = 1; sl < pS; ++sl) {
+            lo += *reinterpret_cast<const f4 *>(q + (size_t)sl * T * pNP);
+            hi += *reinterpret_cast<const f4 *>(q + (size_t)sl * T * pNP + 4);
+          }
+          uint16_t hb[8];
+#pragma unroll
+          for (int q4 = 0; q4 < 4; ++q4) {
+            hb[q4] = f2h_(lo[q4]);
+            hb[q4 + 4] = f2h_(hi[q4]);
+          }
+          xb = *reinterpret_cast<uint4 *>(hb);
+        } else {
+          xb = *reinterpret_cast<const uint4 *>(b + ch * 8);
+        }
         const __half2 *pa = reinterpret_cast<const __half2 *>(&xa);
         const __half2 *pb = reinterpret_cast<const __half2 *>(&xb);
         __half2 r[4];
@@ -87,7 +106,7 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
 
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s, bool out_packed) {
+                          hipStream_t s, bool out_packed, Partials x2p) {
   if (T <= 0) return hipSuccess;
   if (out_packed && H % 32) return hipErrorInvalidValue;
   const int op = out_packed ? 1 : 0;
@@ -95,16 +114,16 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   const int nchunk = H / 8;
   if (nchunk <= 256)
     hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op);
+                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
   else if (nchunk <= 512)
     hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op);
+                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
   else if (nchunk <= 1024)
     hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op);
+                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
   else
     hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op);
+                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
   return hipGetLastError();
 }
 

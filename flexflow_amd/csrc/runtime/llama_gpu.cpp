@@ -312,46 +312,54 @@ struct LlamaGPU : public ffmi_model {
     int pr = prof_begin(ptail);
     TRY(ffmi_embedding(batch, embed, res, H, s));
     prof_end(pr, EMBED, (double)T * H * 4, 0);
+    ffmi::Partials down_part;
     for (int l = 0; l < c.num_layers; ++l) {
       Layer &L = layers[l];
       const bool on = prof_on(l, T);
       pr = prof_begin(on);
-      const int XP = packed ? FFMI_X_PACKED : 0, YP = packed ? FFMI_Y_PACKED : 0;
-      TRY(ffmi_rmsnorm_ex(res, l == 0 ? nullptr : proj, L.in_norm, res, h, T, H, eps, YP, s));
+      // split-K GEMMs leave their partial slabs for the next kernel to combine
+      // (rope-store for qkv; the residual norm for o/down when there is no
+      // all-reduce in between) instead of a separate reduce pass
+      const int XP = packed ? FFMI_X_PACKED : 0;
+      FFMI_HIP(ffmi::launch_rmsnorm(res, l == 0 ? nullptr : proj, L.in_norm, res, h, T, H, eps,
+                                    stream, packed, l == 0 ? ffmi::Partials() : down_part));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 2 : 4), 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(h, L.wqkv, qkv, T, 3 * Hl, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
+      ffmi::Partials qkv_part;
+      FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
+                                 &qkv_part));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
       pr = prof_begin(on);
-      if (mode == FFMI_MODEL_TREE)
-        TRY(ffmi_attn_tree(L.attn, batch, qkv, att, s));
-      else if (mode == FFMI_MODEL_BEAM)
-        TRY(ffmi_attn_spec(L.attn, batch, qkv, att, s));
-      else
-        TRY(ffmi_attn_inc(L.attn, batch, qkv, att, s));
+      TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(att, L.wo, proj, T, H, Hl, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
+      ffmi::Partials o_part;
+      FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
+                                 o.tp_size == 1 ? &o_part : nullptr));
       prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
       prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
       pr = prof_begin(on);
-      TRY(ffmi_rmsnorm_ex(res, proj, L.post_norm, res, h, T, H, eps, YP, s));
+      FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
+                                    o_part));
       prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
       pr = prof_begin(on);
+      const int YP = packed ? FFMI_Y_PACKED : 0;
       TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       pr = prof_begin(on);
-      TRY(ffmi_linear_ws(mlp, L.wd, proj, T, H, Fl, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
+      FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
+                                 o.tp_size == 1 ? &down_part : nullptr));
       prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
       prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
     }
-    const int XP = packed ? FFMI_X_PACKED : 0, YP = packed ? FFMI_Y_PACKED : 0;
+    const int XP = packed ? FFMI_X_PACKED : 0;
     pr = prof_begin(ptail);
-    TRY(ffmi_rmsnorm_ex(res, proj, final_norm, res, h, T, H, eps, YP, s));
+    FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
+                                  down_part));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
     pr = prof_begin(ptail);
     TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));

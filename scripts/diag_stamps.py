@@ -26,11 +26,13 @@ for name, N, K, T in [("qkv", 12288, 4096, 168), ("down", 4096, 11008, 168),
         c = Buf.empty((nb // 2,), np.uint16)
         F.check(L.ffmi_linear_pack_weight(wb.ptr, N, K, c.ptr, None))
         copies.append(c)
-    X = Buf(rng.standard_normal((T, K)).astype(np.float16))
+    X0 = Buf(rng.standard_normal((T, K)).astype(np.float16))
+    X = Buf.empty((L.ffmi_packed_activation_bytes(T, K) // 2,), np.uint16)
+    F.check(L.ffmi_pack_activations(X0.ptr, T, K, X.ptr, None))
     Y = Buf.empty((T, N), np.float16)
     for i in range(len(copies)):
-        F.check(L.ffmi_linear(X.ptr, copies[i].ptr, Y.ptr, T, N, K, 0, None))
-    F.check(L.ffmi_linear(X.ptr, copies[0].ptr, Y.ptr, T, N, K, 0, None))
+        F.check(L.ffmi_linear(X.ptr, copies[i].ptr, Y.ptr, T, N, K, F.X_PACKED, None))
+    F.check(L.ffmi_linear(X.ptr, copies[0].ptr, Y.ptr, T, N, K, F.X_PACKED, None))
     buf = np.zeros((1 << 16, 6), np.int64)
     n = L.ffmi_debug_gemm_stamps(buf.ctypes.data, buf.shape[0])
     st = buf[:n]

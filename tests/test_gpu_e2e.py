@@ -61,6 +61,29 @@ def test_incr_decoding_tokens_match_oracle(cfg, seed):
         check_tokens_vs_oracle(cfg, seed, r.output_tokens, len(p) + 1)
 
 
+def test_long_prompts_exercise_split_k_paths():
+    """Prompts of 70-120 tokens in one 256-token batch put every GEMM on the
+    M-split path with split-K, whose partial slabs are combined by the
+    consumer (rope-store, residual norm): tokens must still match the oracle,
+    and SpecInfer (verify batches > 64 tokens) must equal incr decoding."""
+    cfg, seed = LLM_CFG, 23
+    V = cfg["vocab_size"]
+    ps = prompts(3, V, 70, 120, seed)
+    kw = dict(max_requests_per_batch=4, max_tokens_per_batch=256, max_sequence_length=256)
+    llm = fa.Model(cfg, "inc", max_requests=4, max_tokens=256, max_seq_len=256, weight_seed=seed)
+    res = fa.generate(fa.RequestManager(**kw), llm, ps, max_length=150)
+    for p, r in zip(ps, res):
+        check_tokens_vs_oracle(cfg, seed, r.output_tokens, len(p) + 1)
+    tree = fa.Model(cfg, "tree", max_requests=4, max_tokens=256 + 23 * 4, max_seq_len=256,
+                    max_tree_tokens=23, weight_seed=seed)
+    ssm = fa.Model(cfg, "beam", max_requests=4, max_tokens=256 + 23 * 4, max_seq_len=256,
+                   max_tree_tokens=23, weight_seed=seed)  # SSM == LLM: long accepted paths
+    rm = fa.RequestManager(spec_tree_width=(1, 1, 3), max_spec_tree_token_num=23, **kw)
+    rm.register_ssm_model(ssm)
+    spec = fa.generate(rm, tree, ps, max_length=150, spec=True)
+    assert [r.output_tokens for r in spec] == [r.output_tokens for r in res]
+
+
 def test_incr_decoding_matches_golden_fixture_model():
     # the HF-pinned fixture model (oracle fp32 == HF greedy); GPU fp16 vs oracle fp16
     cfg, g = O.load_golden("tiny_d128")
