@@ -226,6 +226,7 @@ def main():
     t0 = time.time()
     new_tokens, lats, llm_steps, ssm_steps = 0, [], 0, 0
     committed, req_verifies = 0, 0
+    llm_us, ssm_us, wall_us = 0.0, 0.0, 0.0
     for _ in range(args.steps):
         n, lat, res = run_generate(rm, llm, prompts, max_len, spec)
         st = rm.stats()
@@ -235,6 +236,9 @@ def main():
         ssm_steps += st.ssm_steps
         committed += st.tokens_committed
         req_verifies += st.request_verifies
+        llm_us += st.llm_us
+        ssm_us += st.ssm_us
+        wall_us += st.wall_us
     device_sync()
     ctrl.barrier()
     elapsed = ctrl.max(time.time() - t0)
@@ -260,6 +264,11 @@ def main():
         "llm_steps_per_generate": llm_steps / args.steps,
         "ssm_steps_per_generate": ssm_steps / args.steps,
         "init_s": round(init_s, 1),
+        # where a generate's wall time goes (host timers around the model steps)
+        "time_split_ms_per_generate": {
+            "llm_steps": round(llm_us / 1e3 / args.steps, 1),
+            "ssm_steps": round(ssm_us / 1e3 / args.steps, 1),
+            "host_scheduling": round((wall_us - llm_us - ssm_us) / 1e3 / args.steps, 1)},
     }
     if spec:
         # tokens each request commits per verify step (incl. the bonus token)

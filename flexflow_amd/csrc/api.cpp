@@ -75,9 +75,10 @@ extern "C" void ffmi_batch_destroy(ffmi_batch_dev *b) {
   delete b;
 }
 
-extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_desc *d,
-                                         ffmi_stream stream) {
-  FFMI_CHECK(b && d, FFMI_ERR_INVALID);
+namespace ffmi {
+// Host half of the upload: fill the pinned staging blob; returns its size.
+ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *bytes) {
+  FFMI_CHECK(b && d && bytes, FFMI_ERR_INVALID);
   FFMI_CHECK(d->num_tokens >= 0 && d->num_tokens <= b->max_tokens, FFMI_ERR_INVALID);
   FFMI_CHECK(d->num_work >= 0 && d->num_work <= b->max_tokens, FFMI_ERR_INVALID);
   FFMI_CHECK(d->num_commits >= 0 && d->num_commits <= b->max_tokens, FFMI_ERR_INVALID);
@@ -119,13 +120,29 @@ extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_des
   h.off_masks = (int)off;
   memcpy(b->host, &h, sizeof(h));
   FFMI_CHECK(off <= b->cap, FFMI_ERR_INVALID);
-  FFMI_HIP(hipMemcpyAsync(b->dev, b->host, off, hipMemcpyHostToDevice, (hipStream_t)stream));
-  FFMI_HIP(hipEventRecord(b->uploaded, (hipStream_t)stream));
   b->num_tokens = d->num_tokens;
   b->num_work = d->num_work;
   b->num_commits = d->num_commits;
   b->num_mask_reqs = d->num_mask_reqs;
+  *bytes = off;
   return FFMI_OK;
+}
+
+// Device half: one async H2D copy of the staged bytes (capturable in a graph;
+// record_event guards the staging against the next stage call).
+ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool record_event) {
+  FFMI_HIP(hipMemcpyAsync(b->dev, b->host, bytes, hipMemcpyHostToDevice, s));
+  if (record_event) FFMI_HIP(hipEventRecord(b->uploaded, s));
+  return FFMI_OK;
+}
+}  // namespace ffmi
+
+extern "C" ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_desc *d,
+                                         ffmi_stream stream) {
+  size_t bytes = 0;
+  const ffmi_status st = ffmi::batch_stage(b, d, &bytes);
+  if (st != FFMI_OK) return st;
+  return ffmi::batch_copy(b, bytes, (hipStream_t)stream, true);
 }
 
 // ---------------------------------------------------------------------------

@@ -137,6 +137,8 @@ struct ffmi_batch_dev {
 // Internal entry points used by the in-library model runtime (llama_gpu.cpp):
 // the public ffmi_attn_* / ffmi_rmsnorm_ex with deferred split-K inputs.
 namespace ffmi {
+ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *bytes);
+ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool record_event);
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
                          void *out, ffmi_stream stream);
 }  // namespace ffmi

@@ -309,9 +309,11 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     int NTILES, int S, int yp) {
   long long st0 = 0, st1 = 0, st2 = 0;
   if (STAMP) st0 = rt_now();
-  static_assert(NTW % 4 == 0, "NTW pieces are spread over 4 waves");
+  static_assert(NTW % 2 == 0, "gate/up tiles come in pairs");
   static_assert(PF >= 2, "ring depth");
-  constexpr int PPT = NTW / 4;
+  // weight tiles j = wave + 4p are loaded by wave (j % 4); with NTW % 4 != 0
+  // the last round is loaded by the first NTW % 4 waves only
+  constexpr int PPT = (NTW + 3) / 4;
   __shared__ __attribute__((aligned(16))) h8 sB[2][NTW][64];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -365,10 +367,11 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < MTW; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
+        if (NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
     }
 #pragma unroll
-    for (int p = 0; p < PPT; ++p) sB[0][bj[p]][lane] = bq[0][p];
+    for (int p = 0; p < PPT; ++p)
+      if (NTW % 4 == 0 || bj[p] < NTW) sB[0][bj[p]][lane] = bq[0][p];
     __syncthreads();
     if (STAMP) st1 = rt_now();
     // one k-step on ring slot Q; MFMAs read the slot in place, then it is
@@ -390,10 +393,11 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < MTW; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
+        if (NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
       // B(kt+1) lives in ring slot (Q+1) % PF
 #pragma unroll
-      for (int p = 0; p < PPT; ++p) sB[cur ^ 1][bj[p]][lane] = bq[(Q + 1) % PF][p];
+      for (int p = 0; p < PPT; ++p)
+        if (NTW % 4 == 0 || bj[p] < NTW) sB[cur ^ 1][bj[p]][lane] = bq[(Q + 1) % PF][p];
       __syncthreads();
       cur ^= 1;
     };
@@ -491,9 +495,9 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   double best = 1e30;
   p.NTW = 8, p.S = 1;
   // measured k-step times (us) at MTW = 3, packed activations (diag_stamps.py)
-  static const int ntw_opts[3] = {8, 12, 16};
-  static const double base[3] = {0.40, 0.65, 0.90};
-  for (int o = 0; o < 3; ++o) {
+  static const int ntw_opts[4] = {6, 8, 12, 16};
+  static const double base[4] = {0.36, 0.40, 0.65, 0.90};
+  for (int o = 0; o < 4; ++o) {
     const int ntw = ntw_opts[o];
     const int nblk = (ntiles + ntw - 1) / ntw;
     for (int S = 1; S <= 8 && S <= KT; ++S) {
@@ -587,10 +591,12 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
     if (p.MTW == 3) {
       if (p.NTW == 16) FFMI_RUN(3, 16);
       if (p.NTW == 12) FFMI_RUN(3, 12);
+      if (p.NTW == 6) FFMI_RUN(3, 6);
       FFMI_RUN(3, 8);
     }
     if (p.NTW == 16) FFMI_RUN(2, 16);
     if (p.NTW == 12) FFMI_RUN(2, 12);
+    if (p.NTW == 6) FFMI_RUN(2, 6);
     FFMI_RUN(2, 8);
 #undef FFMI_RUN
   }

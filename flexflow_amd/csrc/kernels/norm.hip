@@ -271,25 +271,30 @@ __global__ __launch_bounds__(512) void softmax_topk_reg_kernel(
   float sum = 0.f;
 #pragma unroll
   for (int q = 0; q < 8; ++q) sum += fscratch[q];
-  int chosen[4] = {-1, -1, -1, -1};
+  // p_i = fp16(exp(x_i - max) / sum), computed once and kept in place of the
+  // logits; a selected element is marked 0xFFFF (a NaN pattern p never takes)
+  uint16_t *ph = reinterpret_cast<uint16_t *>(r);
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      ph[v * 8 + e] = (v * 512 + tid) * 8 + e < V
+                          ? f2h_(__fdiv_rn(expf(h2f_(ph[v * 8 + e]) - mx), sum))
+                          : (uint16_t)0xFFFF;
   for (int rd = 0; rd < k; ++rd) {
+    // key = (p + 1) << 32 | ~idx: max key = largest p, then lowest index
     unsigned long long best = 0;
 #pragma unroll
-    for (int v = 0; v < NV; ++v) {
-      const int base = (v * 512 + tid) * 8;
-      if (base >= V) continue;
+    for (int v = 0; v < NV; ++v)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const int i = base + e;
-        bool taken = false;
-        for (int q = 0; q < rd; ++q) taken |= (chosen[q] == i);
-        if (taken) continue;
-        const uint16_t p = f2h_(__fdiv_rn(expf(elem(v, e) - mx), sum));
+        const uint16_t p = ph[v * 8 + e];
+        const unsigned i = (unsigned)((v * 512 + tid) * 8 + e);
         const unsigned long long key =
-            ((unsigned long long)p << 32) | (unsigned long long)(0xffffffffu - (unsigned)i);
+            p == 0xFFFF ? 0ull
+                        : ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
         best = key > best ? key : best;
       }
-    }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       unsigned long long other = __shfl_xor(best, o);
@@ -301,11 +306,20 @@ __global__ __launch_bounds__(512) void softmax_topk_reg_kernel(
     unsigned long long b = kscratch[0];
 #pragma unroll
     for (int q = 1; q < 8; ++q) b = kscratch[q] > b ? kscratch[q] : b;
-    const int idx = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
-    chosen[rd] = idx;
+    const unsigned idx = 0xffffffffu - (unsigned)(b & 0xffffffffu);
+    const uint16_t pbest = (uint16_t)((b >> 32) - 1u);
     if (tid == 0) {
-      ids[(size_t)row * k + rd] = idx;
-      if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)(b >> 32));
+      ids[(size_t)row * k + rd] = (int)idx;
+      if (probs) probs[(size_t)row * k + rd] = h2f_(pbest);
+    }
+    if (rd + 1 < k && (idx >> 3) % 512 == (unsigned)tid) {  // owner marks it taken
+#pragma unroll
+      for (int v = 0; v < NV; ++v)
+        if ((unsigned)(v * 512 + tid) == (idx >> 3)) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e)
+            if ((unsigned)e == (idx & 7)) ph[v * 8 + e] = 0xFFFF;
+        }
     }
   }
 }
@@ -315,17 +329,15 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4) return hipErrorInvalidValue;
   const int nv = (V / 8 + 511) / 512;
-  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 16) {
+  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 8) {
     if (nv <= 1)
       hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
     else if (nv <= 2)
       hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
     else if (nv <= 4)
       hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
-    else if (nv <= 8)
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<8>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
     else
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<16>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+      hipLaunchKernelGGL(softmax_topk_reg_kernel<8>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
   } else {
     hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
   }

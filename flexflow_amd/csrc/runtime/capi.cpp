@@ -126,6 +126,8 @@ extern "C" ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s) {
   s->tokens_committed = rm->rm.stats.tokens_committed;
   s->tree_tokens_verified = rm->rm.stats.tree_tokens_verified;
   s->request_verifies = rm->rm.stats.request_verifies;
+  s->llm_us = rm->rm.stats.llm_us;
+  s->ssm_us = rm->rm.stats.ssm_us;
   s->wall_us = rm->rm.stats.wall_us;
   return FFMI_OK;
 }

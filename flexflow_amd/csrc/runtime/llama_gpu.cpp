@@ -17,6 +17,8 @@
 #include <cmath>
 
 #include <string>
+#include <map>
+#include <tuple>
 #include <vector>
 
 #include "model.h"
@@ -46,7 +48,6 @@ struct LlamaGPU : public ffmi_model {
   uint16_t *res = nullptr, *h = nullptr, *qkv = nullptr, *att = nullptr, *proj = nullptr,
            *mlp = nullptr, *logits = nullptr;
   int32_t *ids_d = nullptr;
-  float *probs_d = nullptr;
   float *ws = nullptr;  // split-K workspace of the GEMMs
   size_t ws_bytes = 0;
   int32_t *ids_h = nullptr;
@@ -153,11 +154,11 @@ struct LlamaGPU : public ffmi_model {
 
   ~LlamaGPU() override {
     if (stream) (void)hipStreamSynchronize(stream);
+    clear_graphs();
     for (auto &L : layers) ffmi_attn_destroy(L.attn);
     for (auto e : ev_pool) (void)hipEventDestroy(e);
     for (void *p : allocs) (void)hipFree(p);
     if (ids_h) (void)hipHostFree(ids_h);
-    if (probs_h) (void)hipHostFree(probs_h);
     ffmi_batch_destroy(batch);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -196,7 +197,7 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&proj, (size_t)Tm * H));
     TRY(alloc(&mlp, (size_t)Tm * Fl));
     TRY(alloc(&logits, (size_t)Tm * V));
-    TRY(alloc(&ids_d, (size_t)Tm * 4));
+    TRY(alloc(&ids_d, (size_t)Tm * 4 * 2));  // [ids | probs] of a step, one D2H copy
     {
       // the split-K factor depends on the row-block count, so take the max
       // over every batch size the model can see
@@ -210,9 +211,7 @@ struct LlamaGPU : public ffmi_model {
       }
       if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
     }
-    TRY(alloc(&probs_d, (size_t)Tm * 4));
-    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * sizeof(int32_t), 0));
-    FFMI_HIP(hipHostMalloc((void **)&probs_h, (size_t)Tm * 4 * sizeof(float), 0));
+    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * 2 * sizeof(int32_t), 0));
     // weights (seeded synthetic, orc_gen_weight spec), packed for MFMA
     uint16_t *tmp = nullptr;
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
@@ -295,19 +294,76 @@ struct LlamaGPU : public ffmi_model {
     return ffmi_allreduce(o.comm, buf, buf, n, FFMI_F16, (ffmi_stream)stream);
   }
 
-  // one step of the graph over the uploaded batch; k = results per token
+  // One step over the packed batch; k = results per token.  Small batches
+  // (SSM beam steps, decode) are launch-bound -- ~20 kernels of a few us
+  // each -- so their whole step (metadata copy, kernels, result copies) is
+  // captured once per batch shape into a HIP graph and replayed.
+  struct GraphKey {
+    int T, W, C, k;
+    size_t bytes;
+    bool operator<(const GraphKey &o) const {
+      return std::tie(T, W, C, k, bytes) < std::tie(o.T, o.W, o.C, o.k, o.bytes);
+    }
+  };
+  std::map<GraphKey, hipGraphExec_t> graphs;
+  bool use_graphs = getenv("FFMI_NO_GRAPHS") == nullptr;
+
   ffmi_status forward(int k) {
+    const int T = (int)ps.tokens.size();
+    ffmi_batch_desc desc;
+    ps.desc(&desc);
+    size_t bytes = 0;
+    ffmi_status st = ffmi::batch_stage(batch, &desc, &bytes);
+    if (st != FFMI_OK) return st;
+    if (T == 0) return FFMI_OK;
+    probs_h = reinterpret_cast<float *>(ids_h + (size_t)T * k);  // (also on graph replay)
+    const bool graph = use_graphs && T <= 64 && o.tp_size == 1 && !prof_on(0, T) &&
+                       !prof_on(c.num_layers / 2, T);
+    if (graph) {
+      const GraphKey key{T, batch->num_work, batch->num_commits, k, bytes};
+      auto it = graphs.find(key);
+      if (it == graphs.end()) {
+        if (graphs.size() >= 512) clear_graphs();
+        hipGraph_t g = nullptr;
+        FFMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+        st = enqueue(k, bytes, false);
+        const hipError_t ce = hipStreamEndCapture(stream, &g);
+        if (st != FFMI_OK || ce != hipSuccess) {
+          if (g) (void)hipGraphDestroy(g);
+          if (st != FFMI_OK) return st;
+          FFMI_HIP(ce);
+        }
+        hipGraphExec_t ex = nullptr;
+        const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+        (void)hipGraphDestroy(g);
+        FFMI_HIP(ie);
+        it = graphs.emplace(key, ex).first;
+      }
+      FFMI_HIP(hipGraphLaunch(it->second, stream));
+    } else {
+      st = enqueue(k, bytes, true);
+      if (st != FFMI_OK) return st;
+    }
+    FFMI_HIP(hipStreamSynchronize(stream));
+    if (!recs.empty()) prof_collect();
+    return FFMI_OK;
+  }
+
+  void clear_graphs() {
+    for (auto &kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    graphs.clear();
+  }
+
+  // everything a step puts on the stream (no host synchronisation inside)
+  ffmi_status enqueue(int k, size_t blob_bytes, bool record_upload) {
     const int T = (int)ps.tokens.size();
     const int H = c.hidden, V = c.vocab_size;
     const float eps = c.rms_eps;
     const ffmi_stream s = (ffmi_stream)stream;
-    ffmi_batch_desc desc;
-    ps.desc(&desc);
     ffmi_status st;
 #define TRY(x) \
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
-    TRY(ffmi_batch_upload(batch, &desc, s));
-    if (T == 0) return FFMI_OK;
+    TRY(ffmi::batch_copy(batch, blob_bytes, stream, record_upload));
     const bool ptail = prof_on(0, T);
     int pr = prof_begin(ptail);
     TRY(ffmi_embedding(batch, embed, res, H, s));
@@ -365,17 +421,14 @@ struct LlamaGPU : public ffmi_model {
     TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
     pr = prof_begin(ptail);
+    // ids [T*k] then probs [T*k] back to back: one result copy per step
+    float *probs_d = reinterpret_cast<float *>(ids_d + (size_t)T * k);
     if (k == 1)
       TRY(ffmi_argmax(logits, T, V, ids_d, probs_d, s));
     else
       TRY(ffmi_arg_topk(logits, T, V, k, ids_d, probs_d, s));
     prof_end(pr, SAMPLING, (double)T * V * 2, 0);
-    FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * sizeof(int32_t), hipMemcpyDeviceToHost,
-                            stream));
-    FFMI_HIP(hipMemcpyAsync(probs_h, probs_d, (size_t)T * k * sizeof(float),
-                            hipMemcpyDeviceToHost, stream));
-    FFMI_HIP(hipStreamSynchronize(stream));
-    if (!recs.empty()) prof_collect();
+    FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));
 #undef TRY
     return FFMI_OK;
   }

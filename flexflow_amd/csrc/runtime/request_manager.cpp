@@ -864,7 +864,9 @@ ffmi_status RequestManager::serve_incr_decoding(ffmi_model *llm) {
       st = FFMI_ERR_INVALID;  // nothing schedulable but requests remain
       break;
     }
+    const double tl = now_us();
     st = llm->run_inc(*bc, ir);
+    stats.llm_us += now_us() - tl;
     if (st != FFMI_OK) break;
     stats.llm_steps++;
   }
@@ -891,7 +893,9 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
     if (all_done()) break;
     for (size_t s = 0; s < ssm_models.size() && st == FFMI_OK; s++) {
       for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {
+        const double ts = now_us();
         st = ssm_models[s]->run_beam((*beam_vec)[s], beam_ir);
+        stats.ssm_us += now_us() - ts;
         if (st != FFMI_OK) break;
         stats.ssm_steps++;
         (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
@@ -903,7 +907,9 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
       st = FFMI_ERR_INVALID;
       break;
     }
+    const double tl = now_us();
     st = llm->run_tree(*tree_bc, tree_ir);
+    stats.llm_us += now_us() - tl;
     if (st != FFMI_OK) break;
     stats.llm_steps++;
   }

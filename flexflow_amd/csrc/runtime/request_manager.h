@@ -128,6 +128,7 @@ class RequestManager {
     long llm_steps = 0, ssm_steps = 0, tokens_committed = 0, tree_tokens_verified = 0;
     long request_verifies = 0;
     double wall_us = 0;
+    double llm_us = 0, ssm_us = 0;  // wall time inside the model steps (incl. sync)
   } stats;
 
  private:

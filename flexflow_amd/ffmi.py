@@ -96,7 +96,7 @@ class OpStat(ctypes.Structure):
 class ServeStats(ctypes.Structure):
     _fields_ = [("llm_steps", c_long), ("ssm_steps", c_long), ("tokens_committed", c_long),
                 ("tree_tokens_verified", c_long), ("request_verifies", c_long),
-                ("wall_us", c_double)]
+                ("wall_us", c_double), ("llm_us", c_double), ("ssm_us", c_double)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ffmi.h

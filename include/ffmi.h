@@ -313,6 +313,7 @@ typedef struct {
   long llm_steps, ssm_steps, tokens_committed, tree_tokens_verified;
   long request_verifies; /* (request, verify step) pairs that committed tokens */
   double wall_us;
+  double llm_us, ssm_us; /* wall time inside LLM / SSM steps; the rest is host scheduling */
 } ffmi_serve_stats;
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 
