@@ -124,6 +124,13 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
   b->num_work = d->num_work;
   b->num_commits = d->num_commits;
   b->num_mask_reqs = d->num_mask_reqs;
+  b->commit_overlap = false;
+  for (int c = 0; c < d->num_commits && !b->commit_overlap; ++c)
+    for (int t = 0; t < d->num_tokens; ++t)
+      if (d->tokens[t].req == d->commits[c].req && d->tokens[t].store_slot == d->commits[c].depth) {
+        b->commit_overlap = true;
+        break;
+      }
   *bytes = off;
   return FFMI_OK;
 }
@@ -152,6 +159,7 @@ struct ffmi_attn {
   ffmi_attn_cfg cfg;
   int slots = 0;
   uint16_t *kc = nullptr, *vc = nullptr, *qbuf = nullptr, *stage = nullptr;
+  int parity = 0;  // TREE staging half written by the next public-API step
   float *rope = nullptr;
 };
 
@@ -192,7 +200,7 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
             hipMalloc((void **)&h->vc, kv * 2) == hipSuccess &&
             hipMalloc((void **)&h->qbuf, (size_t)cfg->max_tokens * Hl * 2) == hipSuccess;
   if (ok && cfg->mode == FFMI_ATTN_TREE)
-    ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * 2) == hipSuccess;
+    ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * 2 * 2) == hipSuccess;
   std::vector<float> tab;
   rope_table(tab, h->slots, cfg->head_dim, cfg->rope_theta);
   if (ok) ok = hipMalloc((void **)&h->rope, tab.size() * sizeof(float)) == hipSuccess;
@@ -205,7 +213,7 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   // never-written slots must hold finite values
   FFMI_HIP(hipMemset(h->kc, 0, kv * 2));
   FFMI_HIP(hipMemset(h->vc, 0, kv * 2));
-  if (h->stage) FFMI_HIP(hipMemset(h->stage, 0, (size_t)cfg->max_tokens * 2 * Hl * 2));
+  if (h->stage) FFMI_HIP(hipMemset(h->stage, 0, (size_t)cfg->max_tokens * 2 * Hl * 2 * 2));
   FFMI_HIP(hipMemcpy(h->rope, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
   *out = h;
   return FFMI_OK;
@@ -231,18 +239,28 @@ extern "C" ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *
 
 namespace ffmi {
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
-                         void *out, ffmi_stream stream) {
+                         void *out, ffmi_stream stream, int parity) {
   FFMI_CHECK(h && b && (qkv || qkvp.S > 0) && out, FFMI_ERR_INVALID);
   FFMI_CHECK(b->num_tokens <= h->cfg.max_tokens, FFMI_ERR_INVALID);
   const bool tree = h->cfg.mode == FFMI_ATTN_TREE;
   const hipStream_t s = (hipStream_t)stream;
   const int heads = h->cfg.num_heads, d = h->cfg.head_dim;
-  if (tree && b->num_commits > 0)
-    FFMI_HIP(ffmi::launch_commit(b->dev, b->num_commits, h->stage, h->kc, h->vc, heads, d,
-                                 h->slots, s));
-  FFMI_HIP(ffmi::launch_rope_store(b->dev, b->num_tokens, (const uint16_t *)qkv, h->qbuf, h->kc,
-                                   h->vc, tree ? h->stage : nullptr, h->rope, heads, d, h->slots,
-                                   h->slots, s, qkvp));
+  uint16_t *stage_wr = nullptr, *stage_rd = nullptr;
+  int C = 0;
+  if (tree) {
+    if (parity < 0) parity = h->parity, h->parity ^= 1;
+    const size_t half = (size_t)h->cfg.max_tokens * 2 * heads * d;
+    stage_wr = h->stage + (parity ? half : 0);
+    stage_rd = h->stage + (parity ? 0 : half);
+    C = b->num_commits;
+    if (C > 0 && b->commit_overlap) {  // reference order: commit, then store
+      FFMI_HIP(ffmi::launch_commit(b->dev, C, stage_rd, h->kc, h->vc, heads, d, h->slots, s));
+      C = 0;
+    }
+  }
+  FFMI_HIP(ffmi::launch_kv_update(b->dev, b->num_tokens, b->num_work, C, (const uint16_t *)qkv,
+                                  qkvp, h->qbuf, h->kc, h->vc, stage_wr, stage_rd, h->rope, heads,
+                                  d, h->slots, h->slots, s));
   FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, h->qbuf, h->kc, h->vc, (uint16_t *)out,
                                   heads, d, h->slots, h->cfg.qk_scale, s,
                                   h->cfg.out_layout == 1));

@@ -107,10 +107,11 @@ hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
                            size_t n, hipStream_t s);
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
                          float *probs, hipStream_t s);
-hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv,
-                             uint16_t *qbuf, uint16_t *kc, uint16_t *vc,
-                             uint16_t *stage, const float *rope, int heads, int d,
-                             int slots, int max_rope_pos, hipStream_t s, Partials qkvp = {});
+
+hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_t *qkv,
+                            Partials qkvp, uint16_t *qbuf, uint16_t *kc, uint16_t *vc,
+                            uint16_t *stage_wr, const uint16_t *stage_rd, const float *rope,
+                            int heads, int d, int slots, int max_rope_pos, hipStream_t s);
 hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
                          uint16_t *kc, uint16_t *vc, int heads, int d, int slots,
                          hipStream_t s);
@@ -131,6 +132,7 @@ struct ffmi_batch_dev {
   int max_tokens = 0, max_requests = 0;
   // host-visible counts of the last upload (launch geometry)
   int num_tokens = 0, num_work = 0, num_commits = 0, num_mask_reqs = 0;
+  bool commit_overlap = false;  // a commit depth is also a slot this step stores
   hipEvent_t uploaded = nullptr;  // guards reuse of the pinned staging
 };
 
@@ -139,6 +141,8 @@ struct ffmi_batch_dev {
 namespace ffmi {
 ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *bytes);
 ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool record_event);
+// parity: which half of the TREE staging this step writes (commits read the
+// other); -1 = the handle's own alternation (public API calls)
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
-                         void *out, ffmi_stream stream);
+                         void *out, ffmi_stream stream, int parity = -1);
 }  // namespace ffmi

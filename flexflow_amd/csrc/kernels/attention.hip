@@ -39,77 +39,6 @@ namespace ffmi {
 __device__ __forceinline__ float h2f(uint16_t v) { return __half2float(__ushort_as_half(v)); }
 __device__ __forceinline__ uint16_t f2h(float v) { return __half_as_ushort(__float2half_rn(v)); }
 
-// RoPE (HF rotate-half, inc...cu:664-738) + KV store (store_kv_cache
-// inc...cu:35-61 / update_tree_branch_kv_cache_fused tree_inc...cu:433-478 /
-// spec_inc_store_kv_cache spec_inc...cu:311-358) + staging copy for commits.
-__global__ void rope_store_kernel(const char *__restrict__ blob, int T,
-                                  const uint16_t *__restrict__ qkv,
-                                  uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
-                                  uint16_t *__restrict__ vc, uint16_t *__restrict__ stage,
-                                  const float *__restrict__ rope, int heads, int d,
-                                  int slots, int max_rope_pos, const float *__restrict__ part,
-                                  int pS, int pNP) {
-  const int hd = d >> 1;
-  const int ppb = blockDim.x / hd;
-  const int pair = blockIdx.x * ppb + threadIdx.x / hd;
-  const int i = threadIdx.x % hd;
-  if (pair >= T * heads) return;
-  const int t = pair / heads, h = pair % heads;
-  BatchView bv = batch_view(blob);
-  const ffmi_token_info ti = bv.tokens[t];
-  const int Hl = heads * d;
-  // qkv element of this token: the fp16 GEMM output, or the in-order sum of
-  // its deferred split-K slabs rounded to fp16 (the same value)
-  auto qkv_at = [&](int col) -> float {
-    return part ? partials_value(part, pS, pNP, T, t, col)
-                : h2f(qkv[(size_t)t * 3 * Hl + col]);
-  };
-  const int qc = h * d, kc0 = Hl + h * d, vc0 = 2 * Hl + h * d;
-  const int pos = min(max(ti.pos, 0), max_rope_pos - 1);
-  const float c = rope[((size_t)pos * hd + i) * 2 + 0];
-  const float s = rope[((size_t)pos * hd + i) * 2 + 1];
-  float a = qkv_at(qc + i), b = qkv_at(qc + i + hd);
-  const uint16_t q0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
-  const uint16_t q1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
-  a = qkv_at(kc0 + i);
-  b = qkv_at(kc0 + i + hd);
-  const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(a, c), __fmul_rn(b, s)));
-  const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(a, s), __fmul_rn(b, c)));
-  const uint16_t v0 = f2h(qkv_at(vc0 + i)), v1 = f2h(qkv_at(vc0 + i + hd));
-  uint16_t *qo = qbuf + (size_t)t * Hl + h * d;
-  qo[i] = q0;
-  qo[i + hd] = q1;
-  if (ti.store_slot >= 0 && ti.store_slot < slots) {
-    uint16_t *kr = kc + (((size_t)ti.req * heads + h) * slots + ti.store_slot) * d;
-    kr[i] = k0;
-    kr[i + hd] = k1;
-    uint16_t *vt = vc + ((size_t)ti.req * heads + h) * d * slots + ti.store_slot;
-    vt[(size_t)i * slots] = v0;
-    vt[(size_t)(i + hd) * slots] = v1;
-  }
-  if (stage) {
-    uint16_t *st = stage + (size_t)t * 2 * Hl + h * d;
-    st[i] = k0;
-    st[i + hd] = k1;
-    st[Hl + i] = v0;
-    st[Hl + i + hd] = v1;
-  }
-}
-
-hipError_t launch_rope_store(const char *blob, int T, const uint16_t *qkv, uint16_t *qbuf,
-                             uint16_t *kc, uint16_t *vc, uint16_t *stage, const float *rope,
-                             int heads, int d, int slots, int max_rope_pos, hipStream_t s,
-                             Partials qkvp) {
-  if (T <= 0) return hipSuccess;
-  const int hd = d / 2;
-  const int ppb = 256 / hd;
-  const int pairs = T * heads;
-  hipLaunchKernelGGL(rope_store_kernel, dim3((pairs + ppb - 1) / ppb), dim3(ppb * hd), 0, s,
-                     blob, T, qkv, qbuf, kc, vc, stage, rope, heads, d, slots, max_rope_pos,
-                     qkvp.S > 0 ? qkvp.p : nullptr, qkvp.S, qkvp.NP);
-  return hipGetLastError();
-}
-
 // commit_tokens_kernel (tree_inc...cu:335-396): accepted tokens of the
 // previous verify batch move from the staging rows to their depth slot.
 __global__ void commit_kernel(const char *__restrict__ blob, int C,
@@ -134,6 +63,116 @@ hipError_t launch_commit(const char *blob, int C, const uint16_t *stage, uint16_
   if (C <= 0) return hipSuccess;
   hipLaunchKernelGGL(commit_kernel, dim3(C * heads), dim3(64), 0, s, blob, C, stage, kc, vc,
                      heads, d, slots);
+  return hipGetLastError();
+}
+
+// Fused KV update of one step: RoPE (HF rotate-half, inc...cu:664-738) + KV
+// store (store_kv_cache inc...cu:35-61 / update_tree_branch_kv_cache_fused
+// tree_inc...cu:433-478 / spec_inc_store_kv_cache spec_inc...cu:311-358) +
+// staging copy for the next step's commits
+// for each (attention work item = <= 16 consecutive tokens of a request, head),
+// plus the TREE commits of the previous verify batch in extra blocks.
+//  * V goes through LDS so that V^T rows are written as runs of consecutive
+//    slots (16 lanes x 2 B) instead of one 2-byte store per (token, d);
+//  * commits read the OTHER half of the ping-pong staging (stage_rd) than the
+//    one this step writes (stage_wr), so both run in one launch.  The host
+//    launches commits separately first when a commit depth coincides with a
+//    slot this step stores (the reference's commit-then-store order).
+template <int D>
+__global__ __launch_bounds__(16 * D / 2) void kv_update_kernel(
+    const char *__restrict__ blob, int T, int W, int C, const uint16_t *__restrict__ qkv,
+    const float *__restrict__ part, int pS, int pNP, uint16_t *__restrict__ qbuf,
+    uint16_t *__restrict__ kc, uint16_t *__restrict__ vc, uint16_t *__restrict__ stage_wr,
+    const uint16_t *__restrict__ stage_rd, const float *__restrict__ rope, int heads, int slots,
+    int max_rope_pos) {
+  constexpr int HD = D / 2;  // one thread per (token of the item, rotation pair)
+  __shared__ uint16_t sV[D][17];
+  __shared__ int sSlot[16];
+  const int Hl = heads * D;
+  const BatchView bv = batch_view(blob);
+  const int item = blockIdx.x / heads, h = blockIdx.x % heads;
+  if (item >= W) {  // ---- commit block (tree_inc...cu:335-396)
+    const int ci = item - W;
+    if (ci >= C) return;
+    const ffmi_commit_info cm = bv.commits[ci];
+    if (cm.depth < 0 || cm.depth >= slots) return;
+    const uint16_t *st = stage_rd + (size_t)cm.src_token * 2 * Hl + h * D;
+    const int i = threadIdx.x;
+    if (i < D) {
+      kc[(((size_t)cm.req * heads + h) * slots + cm.depth) * D + i] = st[i];
+      vc[(((size_t)cm.req * heads + h) * D + i) * slots + cm.depth] = st[Hl + i];
+    }
+    return;
+  }
+  const ffmi_attn_work w = bv.work[item];
+  const int tl = threadIdx.x / HD, i = threadIdx.x % HD;
+  if (tl < w.q_count) {
+    const int t = w.q_start + tl;
+    const ffmi_token_info ti = bv.tokens[t];
+    auto qkv_at = [&](int col) -> float {
+      return part ? partials_value(part, pS, pNP, T, t, col)
+                  : h2f(qkv[(size_t)t * 3 * Hl + col]);
+    };
+    const int qc = h * D, kc0 = Hl + h * D, vc0 = 2 * Hl + h * D;
+    const float qa = qkv_at(qc + i), qb = qkv_at(qc + i + HD);
+    const float ka = qkv_at(kc0 + i), kb = qkv_at(kc0 + i + HD);
+    const float va = qkv_at(vc0 + i), vb = qkv_at(vc0 + i + HD);
+    const int pos = min(max(ti.pos, 0), max_rope_pos - 1);
+    const float c = rope[((size_t)pos * HD + i) * 2 + 0];
+    const float s = rope[((size_t)pos * HD + i) * 2 + 1];
+    const uint16_t q0 = f2h(__fsub_rn(__fmul_rn(qa, c), __fmul_rn(qb, s)));
+    const uint16_t q1 = f2h(__fadd_rn(__fmul_rn(qa, s), __fmul_rn(qb, c)));
+    const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(ka, c), __fmul_rn(kb, s)));
+    const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(ka, s), __fmul_rn(kb, c)));
+    const uint16_t v0 = f2h(va), v1 = f2h(vb);
+    uint16_t *qo = qbuf + (size_t)t * Hl + h * D;
+    qo[i] = q0;
+    qo[i + HD] = q1;
+    const bool store = ti.store_slot >= 0 && ti.store_slot < slots;
+    if (store) {
+      uint16_t *kr = kc + (((size_t)ti.req * heads + h) * slots + ti.store_slot) * D;
+      kr[i] = k0;
+      kr[i + HD] = k1;
+    }
+    if (i == 0) sSlot[tl] = store ? ti.store_slot : -1;
+    sV[i][tl] = v0;
+    sV[i + HD][tl] = v1;
+    if (stage_wr) {
+      uint16_t *st = stage_wr + (size_t)t * 2 * Hl + h * D;
+      st[i] = k0;
+      st[i + HD] = k1;
+      st[Hl + i] = v0;
+      st[Hl + i + HD] = v1;
+    }
+  }
+  __syncthreads();
+  // ---- V^T[req][h][d][slot]: lanes run over consecutive tokens of a d-row
+  uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
+  for (int e = threadIdx.x; e < D * 16; e += blockDim.x) {
+    const int dd = e >> 4, tt = e & 15;
+    if (tt >= w.q_count) continue;
+    const int sl = sSlot[tt];
+    if (sl >= 0) vt[(size_t)dd * slots + sl] = sV[dd][tt];
+  }
+}
+
+hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_t *qkv,
+                            Partials qkvp, uint16_t *qbuf, uint16_t *kc, uint16_t *vc,
+                            uint16_t *stage_wr, const uint16_t *stage_rd, const float *rope,
+                            int heads, int d, int slots, int max_rope_pos, hipStream_t s) {
+  if (W <= 0 && C <= 0) return hipSuccess;
+  const dim3 grid((W + C) * heads);
+  const float *pp = qkvp.S > 0 ? qkvp.p : nullptr;
+  if (d == 128)
+    hipLaunchKernelGGL(kv_update_kernel<128>, grid, dim3(1024), 0, s, blob, T, W, C, qkv, pp,
+                       qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
+                       max_rope_pos);
+  else if (d == 64)
+    hipLaunchKernelGGL(kv_update_kernel<64>, grid, dim3(512), 0, s, blob, T, W, C, qkv, pp,
+                       qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
+                       max_rope_pos);
+  else
+    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -299,12 +299,17 @@ struct LlamaGPU : public ffmi_model {
   // each -- so their whole step (metadata copy, kernels, result copies) is
   // captured once per batch shape into a HIP graph and replayed.
   struct GraphKey {
-    int T, W, C, k;
+    int T, W, C, k, parity, overlap;
     size_t bytes;
     bool operator<(const GraphKey &o) const {
-      return std::tie(T, W, C, k, bytes) < std::tie(o.T, o.W, o.C, o.k, o.bytes);
+      return std::tie(T, W, C, k, parity, overlap, bytes) <
+             std::tie(o.T, o.W, o.C, o.k, o.parity, o.overlap, o.bytes);
     }
   };
+  // TREE steps write alternate halves of the attention staging (commits of
+  // the next step read the half this one wrote); kept here so graph replays
+  // and eager steps agree
+  int tree_parity = 0;
   std::map<GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = getenv("FFMI_NO_GRAPHS") == nullptr;
 
@@ -320,7 +325,8 @@ struct LlamaGPU : public ffmi_model {
     const bool graph = use_graphs && T <= 64 && o.tp_size == 1 && !prof_on(0, T) &&
                        !prof_on(c.num_layers / 2, T);
     if (graph) {
-      const GraphKey key{T, batch->num_work, batch->num_commits, k, bytes};
+      const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
+                         batch->commit_overlap ? 1 : 0, bytes};
       auto it = graphs.find(key);
       if (it == graphs.end()) {
         if (graphs.size() >= 512) clear_graphs();
@@ -345,6 +351,7 @@ struct LlamaGPU : public ffmi_model {
       if (st != FFMI_OK) return st;
     }
     FFMI_HIP(hipStreamSynchronize(stream));
+    if (mode == FFMI_MODEL_TREE) tree_parity ^= 1;
     if (!recs.empty()) prof_collect();
     return FFMI_OK;
   }
@@ -386,7 +393,8 @@ struct LlamaGPU : public ffmi_model {
                                  &qkv_part));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
       pr = prof_begin(on);
-      TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s));
+      TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s,
+                             mode == FFMI_MODEL_TREE ? tree_parity : -1));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
       pr = prof_begin(on);
       ffmi::Partials o_part;
