@@ -1,12 +1,15 @@
 // api.cpp -- C ABI of the kernel-level boundary (include/ffmi.h).
 #include <rccl/rccl.h>
 #include <stdio.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
+
+#include <algorithm>
 
 #include "ffmi_internal.h"
 
@@ -124,6 +127,14 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
   b->num_work = d->num_work;
   b->num_commits = d->num_commits;
   b->num_mask_reqs = d->num_mask_reqs;
+  b->max_q = 0;
+  b->one_item_per_req = true;
+  for (int wi = 0; wi < d->num_work; ++wi) {
+    FFMI_CHECK(d->work[wi].q_count >= 0 && d->work[wi].q_count <= FFMI_ATTN_QTILE,
+               FFMI_ERR_INVALID);
+    b->max_q = std::max(b->max_q, (int)d->work[wi].q_count);
+    if (wi > 0 && d->work[wi].req == d->work[wi - 1].req) b->one_item_per_req = false;
+  }
   b->commit_overlap = false;
   for (int c = 0; c < d->num_commits && !b->commit_overlap; ++c)
     for (int t = 0; t < d->num_tokens; ++t)
@@ -253,17 +264,30 @@ ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
     stage_wr = h->stage + (parity ? half : 0);
     stage_rd = h->stage + (parity ? 0 : half);
     C = b->num_commits;
+  }
+  // One workgroup per request with few tokens (decode, SSM beam steps):
+  // commits + KV update + attention in one launch (the workgroup orders
+  // commit before store itself).  Larger items (tree verify, prefill) keep
+  // the separate KV-update launch: a 256-thread prologue over 16+ tokens
+  // costs more latency than the launch it saves (measured on 7B verify).
+  // FFMI_ATTN_NO_FUSE=1 forces the two-launch path (A/B and parity tests).
+  const bool fused = b->one_item_per_req && b->max_q <= 8 &&
+                     getenv("FFMI_ATTN_NO_FUSE") == nullptr;
+  if (!fused) {
     if (C > 0 && b->commit_overlap) {  // reference order: commit, then store
       FFMI_HIP(ffmi::launch_commit(b->dev, C, stage_rd, h->kc, h->vc, heads, d, h->slots, s));
       C = 0;
     }
+    FFMI_HIP(ffmi::launch_kv_update(b->dev, b->num_tokens, b->num_work, C,
+                                    (const uint16_t *)qkv, qkvp, h->qbuf, h->kc, h->vc, stage_wr,
+                                    stage_rd, h->rope, heads, d, h->slots, h->slots, s));
+    C = 0;
   }
-  FFMI_HIP(ffmi::launch_kv_update(b->dev, b->num_tokens, b->num_work, C, (const uint16_t *)qkv,
-                                  qkvp, h->qbuf, h->kc, h->vc, stage_wr, stage_rd, h->rope, heads,
-                                  d, h->slots, h->slots, s));
-  FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, h->qbuf, h->kc, h->vc, (uint16_t *)out,
-                                  heads, d, h->slots, h->cfg.qk_scale, s,
-                                  h->cfg.out_layout == 1));
+  FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, b->max_q, h->qbuf, h->kc, h->vc,
+                                  (uint16_t *)out, heads, d, h->slots, h->cfg.qk_scale, s,
+                                  h->cfg.out_layout == 1, fused, b->num_tokens, C,
+                                  (const uint16_t *)qkv, qkvp, stage_wr, stage_rd, h->rope,
+                                  h->slots));
   return FFMI_OK;
 }
 }  // namespace ffmi

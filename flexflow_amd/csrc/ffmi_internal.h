@@ -115,10 +115,11 @@ hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_
 hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
                          uint16_t *kc, uint16_t *vc, int heads, int d, int slots,
                          hipStream_t s);
-hipError_t launch_attention(const char *blob, int W, const uint16_t *qbuf,
-                            const uint16_t *kc, const uint16_t *vc, uint16_t *out,
-                            int heads, int d, int slots, float scale, hipStream_t s,
-                            bool out_packed = false);
+hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, uint16_t *kc,
+                            uint16_t *vc, uint16_t *out, int heads, int d, int slots, float scale,
+                            hipStream_t s, bool out_packed, bool fused, int T, int C,
+                            const uint16_t *qkv, Partials qkvp, uint16_t *stage_wr,
+                            const uint16_t *stage_rd, const float *rope, int max_rope_pos);
 
 uint64_t weight_key(const char *name, uint64_t seed);
 
@@ -133,6 +134,8 @@ struct ffmi_batch_dev {
   // host-visible counts of the last upload (launch geometry)
   int num_tokens = 0, num_work = 0, num_commits = 0, num_mask_reqs = 0;
   bool commit_overlap = false;  // a commit depth is also a slot this step stores
+  bool one_item_per_req = false;  // every request's tokens form one attention work item
+  int max_q = 0;                  // largest work item
   hipEvent_t uploaded = nullptr;  // guards reuse of the pinned staging
 };
 

@@ -299,11 +299,11 @@ struct LlamaGPU : public ffmi_model {
   // each -- so their whole step (metadata copy, kernels, result copies) is
   // captured once per batch shape into a HIP graph and replayed.
   struct GraphKey {
-    int T, W, C, k, parity, overlap;
+    int T, W, C, k, parity, overlap, fused, max_q;
     size_t bytes;
     bool operator<(const GraphKey &o) const {
-      return std::tie(T, W, C, k, parity, overlap, bytes) <
-             std::tie(o.T, o.W, o.C, o.k, o.parity, o.overlap, o.bytes);
+      return std::tie(T, W, C, k, parity, overlap, fused, max_q, bytes) <
+             std::tie(o.T, o.W, o.C, o.k, o.parity, o.overlap, o.fused, o.max_q, o.bytes);
     }
   };
   // TREE steps write alternate halves of the attention staging (commits of
@@ -326,7 +326,8 @@ struct LlamaGPU : public ffmi_model {
                        !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
-                         batch->commit_overlap ? 1 : 0, bytes};
+                         batch->commit_overlap ? 1 : 0, batch->one_item_per_req ? 1 : 0,
+                         batch->max_q, bytes};
       auto it = graphs.find(key);
       if (it == graphs.end()) {
         if (graphs.size() >= 512) clear_graphs();

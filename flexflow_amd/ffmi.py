@@ -22,7 +22,7 @@ EPI_NONE, EPI_SILU_MUL = 0, 1
 X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
 Y_PACKED = 0x20  # FFMI_Y_PACKED
 F16, F32, I32 = 0, 1, 2
-ATTN_QTILE = 16
+ATTN_QTILE = 32
 MAX_TREE = 64
 
 

@@ -81,7 +81,7 @@ typedef struct {
   int32_t pad;
 } ffmi_commit_info;
 
-#define FFMI_ATTN_QTILE 16
+#define FFMI_ATTN_QTILE 32
 #define FFMI_MAX_TREE 64
 
 /* Host-side description of one step (pointers into host memory). */

@@ -13,7 +13,7 @@ import pytest
 
 import flexflow_amd.ffmi as F
 import oracle_lib as O
-from hip_util import Buf, f16, sync, ulp_diff
+from hip_util import Buf, f16, hip, sync, ulp_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -352,6 +352,33 @@ def test_attention_inc_prefill_then_decode(d, layout):
     out, qs = c.run(infos, rng=rng)
     for t, i in enumerate(infos):
         close16(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)), exact_frac=0.98)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_attention_fused_equals_two_launch_path(d, monkeypatch):
+    """One workgroup per request (decode / beam / verify steps) runs commits,
+    KV update and attention in one launch; FFMI_ATTN_NO_FUSE=1 runs the
+    separate KV-update kernel first.  Outputs and caches must be identical."""
+    def scenario():
+        rng = np.random.default_rng(77 + d)
+        c = AttnCase(F.ATTN_INC, d=d)
+        lens = {0: 3, 1: 8, 2: 6}   # prefill: one small item per request -> fused
+        infos = [(5, p, r, p, p + 1, 0, 0, 0) for r, n in lens.items() for p in range(n)]
+        o1, _ = c.run(infos, rng=rng)
+        infos = [(7, n, r, n, n + 1, 0, 0, 0) for r, n in lens.items()]   # decode step
+        o2, _ = c.run(infos, rng=rng)
+        k, v = ctypes.c_void_p(), ctypes.c_void_p()
+        slots = ctypes.c_int()
+        F.check(L.ffmi_attn_kv_ptrs(c.h, ctypes.byref(k), ctypes.byref(v), ctypes.byref(slots)))
+        n = 4 * c.heads * slots.value * c.d
+        kc = np.empty(n, np.uint16)
+        hip().hipMemcpy(kc.ctypes.data, k, n * 2, 2)
+        return o1, o2, kc
+    fused = scenario()
+    monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
+    split = scenario()
+    for a, b in zip(fused, split):
+        assert np.array_equal(np.asarray(a).view(np.uint16), np.asarray(b).view(np.uint16))
 
 
 def tree_masks(parents):
