@@ -24,27 +24,44 @@ __device__ __forceinline__ T block_sum256(T v, T *scratch) {
   return r;
 }
 
+template <int NW, typename T>
+__device__ __forceinline__ T block_sum(T v, T *scratch) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) scratch[wave] = v;
+  __syncthreads();
+  T r = scratch[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) r += scratch[q];
+  return r;
+}
+
 // rms_norm_kernels.cu:97-124 / residual_rms_norm_kernels.cu:98-131:
 //   r = x1 (+ x2, rounded to half); rms = half(rsqrt(mean(r^2) + eps));
 //   y = half(r * rms); out = half(y * w)
-template <int MAXC>
-__global__ __launch_bounds__(256) void rmsnorm_kernel(
+// One workgroup of NT threads per row, MAXC 8-element chunks per thread; every
+// load of the row (x1, x2 or its split-K slabs, and w) is issued before the
+// reduction, so a row costs one memory round trip.
+template <int NT, int MAXC>
+__global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
     uint16_t *__restrict__ out, int H, float eps, int out_packed,
     const float *__restrict__ x2p, int pS, int pNP) {
-  __shared__ float scratch[4];
+  __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int T = gridDim.x;
   const int nchunk = H >> 3;
   const uint16_t *a = x1 + (size_t)row * H;
   const uint16_t *b = x2 ? x2 + (size_t)row * H : nullptr;
-  uint4 v[MAXC];
+  uint4 v[MAXC], wv[MAXC];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = threadIdx.x + c * 256;
+    const int ch = threadIdx.x + c * NT;
     if (ch < nchunk) {
+      wv[c] = *reinterpret_cast<const uint4 *>(w + ch * 8);
       uint4 xa = *reinterpret_cast<const uint4 *>(a + ch * 8);
       if (b || x2p) {
         uint4 xb;
@@ -82,16 +99,15 @@ __global__ __launch_bounds__(256) void rmsnorm_kernel(
       }
     }
   }
-  const float sum = block_sum256(ss, scratch);
+  const float sum = block_sum<NT / 64>(ss, scratch);
   const float rms_f = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
   const float rms = h2f_(f2h_(rms_f));
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
-    const int ch = threadIdx.x + c * 256;
+    const int ch = threadIdx.x + c * NT;
     if (ch < nchunk) {
-      uint4 wv = *reinterpret_cast<const uint4 *>(w + ch * 8);
       const uint16_t *e = reinterpret_cast<const uint16_t *>(&v[c]);
-      const uint16_t *we = reinterpret_cast<const uint16_t *>(&wv);
+      const uint16_t *we = reinterpret_cast<const uint16_t *>(&wv[c]);
       uint16_t o8[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -110,20 +126,19 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   if (T <= 0) return hipSuccess;
   if (out_packed && H % 32) return hipErrorInvalidValue;
   const int op = out_packed ? 1 : 0;
-  if (H % 8 != 0 || H > 8 * 256 * 8) return hipErrorInvalidValue;
   const int nchunk = H / 8;
-  if (nchunk <= 256)
-    hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
-  else if (nchunk <= 512)
-    hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
-  else if (nchunk <= 1024)
-    hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
-  else
-    hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, x1, x2, w, res_out, out,
-                       H, eps, op, x2p.S > 0 ? x2p.p : nullptr, x2p.S, x2p.NP);
+  if (nchunk > 4096) return hipErrorInvalidValue;
+  const float *pp = x2p.S > 0 ? x2p.p : nullptr;
+#define FFMI_RMS(NT, MC)                                                                    \
+  hipLaunchKernelGGL((rmsnorm_kernel<NT, MC>), dim3(T), dim3(NT), 0, s, x1, x2, w, res_out, \
+                     out, H, eps, op, pp, x2p.S, x2p.NP)
+  if (nchunk <= 128) FFMI_RMS(128, 1);
+  else if (nchunk <= 256) FFMI_RMS(256, 1);
+  else if (nchunk <= 512) FFMI_RMS(512, 1);
+  else if (nchunk <= 1024) FFMI_RMS(1024, 1);
+  else if (nchunk <= 2048) FFMI_RMS(1024, 2);
+  else FFMI_RMS(1024, 4);
+#undef FFMI_RMS
   return hipGetLastError();
 }
 
