@@ -157,6 +157,23 @@ def cpu_baseline(prompt_len=4, max_steps=96, budget_s=15.0, batch=8):
                        f"after a {prompt_len}-token prompt, {dt:.1f}s")
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of the roofline kernel, measured with rocprofv3
+    --pmc FETCH_SIZE in a separate run (scripts/round_gpu.sh ->
+    scripts/pmc_summary.py -> profiles/rNN_pmc_fetch.json); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_fetch.json")))
+    for f in reversed(files):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        if d.get("kernel") == kernel:
+            d["source"] = os.path.relpath(f, ROOT)
+            return d
+    return None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -285,6 +302,10 @@ def main():
                            "kernel": k, "launches_sampled": g["launches"],
                            "avg_launch_us": round(1000 * g["ms"] / g["launches"], 2),
                            "bytes_per_launch": round(g["bytes"] / g["launches"])}
+        tr = pmc_traffic(k)
+        if tr:
+            out["roofline"]["traffic"] = tr["fetch_bytes_per_launch"]
+            out["roofline"]["traffic_source"] = tr["source"]
         out["op_breakdown_sampled"] = {
             kk: {"avg_us": round(1000 * v["ms"] / v["launches"], 2),
                  "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,
