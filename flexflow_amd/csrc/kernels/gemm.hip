@@ -20,6 +20,7 @@
 //    row's result does not depend on T or on which other rows are batched.
 // Epilogue FFMI_EPI_SILU_MUL fuses SigmoidSiluMulti (sigmoid_silu_multi.cu:
 // 37-47) on interleaved [gate|up] tiles.
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -53,33 +54,26 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
   return __half_as_ushort(__float2half_rn(t * u));
 }
 
-// MULTI = 1: multi-pass over row blocks of MT*16 rows.  The grid is 1-D and
-// XCD-grouped: the row blocks of one column block get linear ids 8 apart
-// (ids are dealt round-robin over the 8 XCDs), so they run together on ONE
-// XCD and the weight tile crosses HBM once and is re-read from that XCD's
-// L2 by the sibling row blocks (MI355X_MICROARCH.md ring-vs-splitk: "tiles
-// with the rows split").
-template <int MT, int NT, int KW, int U, int EPI, int MULTI>
+// Split-K over workgroups (grid.y = S > 1, small-N layers only): each
+// workgroup reduces its K slice over its waves and writes an fp32 partial
+// slab [S][T][NTILES*16] that the consumer combines in slice order
+// (Partials, the M-split kernel's slab layout).
+template <int MT, int NT, int KW, int U, int EPI>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *__restrict__ Y, int T, int N, int K, int KT, int NTILES, int mpasses, int xp,
-    int yp) {
+    uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
+    int NTILES, int xp, int yp) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
-  int cb = blockIdx.x, mb = 0;
-  if (MULTI) {
-    const int grp = 8 * mpasses;
-    const int r = blockIdx.x % grp;
-    cb = (blockIdx.x / grp) * 8 + (r & 7);
-    mb = r >> 3;
-    if (cb * NT >= NTILES) return;
-  }
+  const int cb = blockIdx.x, ks = blockIdx.y, S = gridDim.y;
   const int tile0 = cb * NT;
-  const int m0 = mb * (MT * 16);
-  const int per = (KT + KW - 1) / KW;
-  const int kb = min(KT, wave * per);
-  const int ke = min(KT, kb + per);
+  const int m0 = 0;
+  const int per_wg = (KT + S - 1) / S;
+  const int kb_wg = min(KT, ks * per_wg), ke_wg = min(KT, kb_wg + per_wg);
+  const int per = (ke_wg - kb_wg + KW - 1) / KW;
+  const int kb = min(ke_wg, kb_wg + wave * per);
+  const int ke = min(ke_wg, kb + per);
 
   f4 acc[MT][NT];
 #pragma unroll
@@ -170,6 +164,22 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
   }
 
   // Epilogue: C/D layout col = lane&15, row = (lane>>4)*4 + r.
+  if (S > 1) {  // EPI == 0 only (host-checked)
+    const int NP = NTILES * 16;
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = (tile0 + j) * 16 + (lane & 15);
+      if (tile0 + j >= NTILES) continue;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          if (m < T) Ypart[((size_t)ks * T + m) * NP + n] = acc[i][j][r];
+        }
+    }
+    return;
+  }
   if (EPI == 0) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -202,30 +212,43 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
   }
 }
 
-template <int MT, int NT, int KW, int U, int EPI, int MULTI>
-static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T, int N,
-                      int K, int KT, int NTILES, int mpasses, hipStream_t s, int xp, int yp) {
+template <int MT, int NT, int KW, int U, int EPI>
+static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws, int T,
+                      int N, int K, int KT, int NTILES, int S, hipStream_t s, int xp, int yp) {
   const int ncb = (NTILES + NT - 1) / NT;
-  dim3 grid(MULTI ? (ncb + 7) / 8 * 8 * mpasses : ncb);
+  dim3 grid(ncb, S);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, MULTI>), grid, dim3(KW * 64), lds,
-                     s, X, Wp, Y, T, N, K, KT, NTILES, MULTI ? mpasses : 1, xp, yp);
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI>), grid, dim3(KW * 64), lds, s, X,
+                     Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
   return hipGetLastError();
 }
 
-template <int MT, int U, int MULTI>
-static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T,
-                              int N, int K, int KT, int epi, int mpasses, hipStream_t s,
+// Split-K factor of the skinny path: only narrow layers (few column groups,
+// e.g. the 68M SSM's o/down with 48 tiles) and only when the consumer takes
+// the partial slabs (no reduce pass); keeps >= 4 k-steps per wave.
+static int skinny_split(int T, int N, int K, int epi, bool deferrable) {
+  if (!deferrable || epi || T > 64) return 1;
+  const int ntiles = (N + 15) / 16;
+  if (ntiles >= 128) return 1;
+  const int KT = K / 32;
+  int S = 256 / ntiles;
+  S = std::min(S, std::max(1, KT / 8));  // >= 1 k-step per wave of an 8-wave slice
+  return std::max(1, std::min(S, 8));
+}
+
+template <int MT, int U>
+static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
+                              int T, int N, int K, int KT, int epi, int S, hipStream_t s,
                               int xp = 0, int yp = 0) {
   int ntiles = (N + 15) / 16;
   if (epi == FFMI_EPI_SILU_MUL)
-    return run<MT, 2, 4, U, 1, MULTI>(X, Wp, Y, T, N, K, KT, 2 * ntiles, mpasses, s, xp, yp);
+    return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp);
   if (MT >= 4 && ntiles >= 512)
-    return run<MT, 2, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
+    return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
   // 8-wave groups only where the accumulators fit 2 waves/SIMD (no spills)
   if (ntiles >= 512 || MT >= 8)
-    return run<MT, 1, 4, U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
-  return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0, MULTI>(X, Wp, Y, T, N, K, KT, ntiles, mpasses, s, xp, yp);
+    return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+  return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
 }
 
 // ---------------------------------------------------------------------------
@@ -357,14 +380,15 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
   // Loads retire in issue order (vmcnt), so X must be issued as early as the
   // weights: X(k) is consumed PF steps after issue, B(k+1) goes to the LDS
   // tile PF-1 steps after issue, and no consumer waits on a young load.
-  if (kb < ke) {
+  auto kloop = [&](auto NVc) {
+    constexpr int NV = decltype(NVc)::value;
     h8 bq[PF][PPT];
     h8 xq[PF][MTW];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
       const int kq = min(kb + q, ke - 1);
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
+      for (int i = 0; i < NV; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
         if (NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
@@ -384,13 +408,13 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
 #pragma unroll
       for (int j = 0; j < NTW; ++j) b[j] = sB[cur][j][lane];
 #pragma unroll
-      for (int i = 0; i < MTW; ++i)
+      for (int i = 0; i < NV; ++i)
 #pragma unroll
         for (int j = 0; j < NTW; ++j)  // D = W . X^T (see mid_store)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(b[j], xq[Q][i], acc[i][j], 0, 0, 0);
       const int kw = min(kt + PF, ke - 1);
 #pragma unroll
-      for (int i = 0; i < MTW; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
+      for (int i = 0; i < NV; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
         if (NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
@@ -407,7 +431,8 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     static_for<PF - 1>([&](auto Qc) {  // tail: < PF steps, slots 0..
       if (kt0 + decltype(Qc)::value < ke) step(Qc, kt0 + decltype(Qc)::value);
     });
-  }
+  };
+  if (kb < ke) kloop(std::integral_constant<int, MTW>{});
   if (STAMP) st2 = rt_now();
 
   mid_store<MTW, NTW, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0, m0, lane, yp);
@@ -511,6 +536,14 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
     }
   }
+  // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split
+  static const char *force = getenv("FFMI_GEMM_PLAN");
+  if (force) {
+    int ntw = 0, S = 0;
+    if (sscanf(force, "%d,%d", &ntw, &S) == 2 && (ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) &&
+        S >= 1 && S <= KT)
+      p.NTW = ntw, p.S = S;
+  }
   p.nblk = (ntiles + p.NTW - 1) / p.NTW;
   return p;
 }
@@ -518,7 +551,10 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
   const int mtiles = (T + 15) / 16;
-  if (mtiles <= 4) return 0;
+  if (mtiles <= 4) {
+    const int S = skinny_split(T, N, K, epilogue, true);
+    return S > 1 ? (size_t)S * T * ((N + 15) / 16) * 16 * sizeof(float) : 0;
+  }
   const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
   const int S = std::max(mid_plan(T, N, K, epilogue, false).S,
                          epilogue ? 1 : mid_plan(T, N, K, epilogue, true).S);
@@ -601,9 +637,15 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
 #undef FFMI_RUN
   }
   const int xi = xp ? 1 : 0;
-  if (mtiles <= 1) return dispatch_nt<1, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
-  if (mtiles <= 2) return dispatch_nt<2, 8, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
-  return dispatch_nt<4, 4, 0>(X, Wp, Y, T, N, K, KT, epilogue, 1, s, xi, yp);
+  int S = skinny_split(T, N, K, epilogue, defer != nullptr);
+  const size_t need = (size_t)S * T * ((N + 15) / 16) * 16 * sizeof(float);
+  if (S > 1 && (!ws || ws_bytes < need)) S = 1;
+  hipError_t e;
+  if (mtiles <= 1) e = dispatch_nt<1, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
+  else if (mtiles <= 2) e = dispatch_nt<2, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
+  else e = dispatch_nt<4, 4>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
+  if (S > 1 && e == hipSuccess) defer->p = ws, defer->S = S, defer->NP = (N + 15) / 16 * 16;
+  return e;
 }
 
 // Packed activation tiles: Xp[mt][kt][lane][8] = X[mt*16 + (lane&15)][kt*32 + 8(lane>>4) + e]
