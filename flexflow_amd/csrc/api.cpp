@@ -10,6 +10,7 @@
 #include <vector>
 
 #include <algorithm>
+#include <climits>
 
 #include "ffmi_internal.h"
 
@@ -51,7 +52,7 @@ extern "C" ffmi_status ffmi_batch_create(int max_tokens, int max_requests, ffmi_
   b->max_requests = max_requests;
   // header + tokens + work (<= tokens) + commits (<= tokens) + masks
   b->cap = align16(sizeof(ffmi::BatchHeader)) + align16((size_t)max_tokens * sizeof(ffmi_token_info)) +
-           align16((size_t)max_tokens * sizeof(ffmi_attn_work)) +
+           align16((size_t)max_tokens * sizeof(ffmi::WorkDev)) +
            align16((size_t)max_tokens * sizeof(ffmi_commit_info)) +
            align16((size_t)max_requests * FFMI_MAX_TREE * sizeof(uint64_t)) + 64;
   if (hipHostMalloc((void **)&b->host, b->cap, hipHostMallocDefault) != hipSuccess ||
@@ -89,11 +90,32 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
   // the pinned staging may still be read by the previous async copy
   FFMI_HIP(hipEventSynchronize(b->uploaded));
   ffmi::BatchHeader h;
-  size_t off = align16(sizeof(h));
   h.num_tokens = d->num_tokens;
   h.num_work = d->num_work;
   h.num_commits = d->num_commits;
   h.num_mask_reqs = d->num_mask_reqs;
+  size_t off = ffmi::kBlobWorkOffset;
+  h.off_work = (int)off;
+  {
+    // lowest slot this step writes for each item's request (its stores and
+    // the TREE commits): the attention kernel may load keys below it before
+    // its own KV-update prologue has run
+    ffmi::WorkDev *wd = reinterpret_cast<ffmi::WorkDev *>(b->host + off);
+    for (int wi = 0; wi < d->num_work; ++wi) {
+      ffmi::WorkDev x{};
+      x.w = d->work[wi];
+      int clean = INT32_MAX;
+      for (int t = 0; t < d->num_tokens; ++t)
+        if (d->tokens[t].req == x.w.req && d->tokens[t].store_slot >= 0)
+          clean = std::min(clean, (int)d->tokens[t].store_slot);
+      for (int c = 0; c < d->num_commits; ++c)
+        if (d->commits[c].req == x.w.req && d->commits[c].depth >= 0)
+          clean = std::min(clean, (int)d->commits[c].depth);
+      x.clean = clean;
+      wd[wi] = x;
+    }
+  }
+  off += align16(d->num_work * sizeof(ffmi::WorkDev));
   h.off_tokens = (int)off;
   {
     // kernels read the query-major visibility word; derive it here from the
@@ -112,9 +134,6 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
     }
   }
   off += align16(d->num_tokens * sizeof(ffmi_token_info));
-  h.off_work = (int)off;
-  memcpy(b->host + off, d->work, d->num_work * sizeof(ffmi_attn_work));
-  off += align16(d->num_work * sizeof(ffmi_attn_work));
   h.off_commits = (int)off;
   if (d->num_commits) memcpy(b->host + off, d->commits, d->num_commits * sizeof(ffmi_commit_info));
   off += align16(d->num_commits * sizeof(ffmi_commit_info));
@@ -265,19 +284,19 @@ ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
     stage_rd = h->stage + (parity ? 0 : half);
     C = b->num_commits;
   }
-  // One workgroup per request with few tokens (decode, SSM beam steps):
-  // commits + KV update + attention in one launch (the workgroup orders
-  // commit before store itself).  Larger items (tree verify, prefill) keep
-  // the separate KV-update launch: a 256-thread prologue over 16+ tokens
-  // costs more latency than the launch it saves (measured on 7B verify).
-  // FFMI_ATTN_NO_FUSE=1 forces the two-launch path (A/B and parity tests).
-  const bool fused = b->one_item_per_req && b->max_q <= 8 &&
-                     getenv("FFMI_ATTN_NO_FUSE") == nullptr;
+  // One work item per request (decode, SSM beam steps, tree verify): commits
+  // + KV update + attention in one launch.  Otherwise (prefill blocks) the
+  // separate KV-update launch first.  Commits whose depth coincides with a
+  // slot this step stores go first in their own launch (the reference's
+  // commit-then-store order).  FFMI_ATTN_NO_FUSE=1 forces the two-launch path
+  // (A/B and parity tests).
+  const bool no_fuse = getenv("FFMI_ATTN_NO_FUSE") != nullptr;
+  const bool fused = b->one_item_per_req && !no_fuse;
+  if (C > 0 && b->commit_overlap) {
+    FFMI_HIP(ffmi::launch_commit(b->dev, C, stage_rd, h->kc, h->vc, heads, d, h->slots, s));
+    C = 0;
+  }
   if (!fused) {
-    if (C > 0 && b->commit_overlap) {  // reference order: commit, then store
-      FFMI_HIP(ffmi::launch_commit(b->dev, C, stage_rd, h->kc, h->vc, heads, d, h->slots, s));
-      C = 0;
-    }
     FFMI_HIP(ffmi::launch_kv_update(b->dev, b->num_tokens, b->num_work, C,
                                     (const uint16_t *)qkv, qkvp, h->qbuf, h->kc, h->vc, stage_wr,
                                     stage_rd, h->rope, heads, d, h->slots, h->slots, s));
@@ -520,6 +539,10 @@ extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, s
 
 extern "C" long ffmi_debug_gemm_stamps(long long *dst, long max_waves) {
   return ffmi::gemm_debug_stamps(dst, max_waves);
+}
+
+extern "C" long ffmi_debug_attn_stamps(long long *dst, long max_waves) {
+  return ffmi::attn_debug_stamps(dst, max_waves);
 }
 
 extern "C" size_t ffmi_packed_activation_bytes(int T, int in_dim) {

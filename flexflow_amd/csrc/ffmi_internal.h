@@ -42,16 +42,29 @@ __host__ __device__ __forceinline__ size_t act_packed_off(int m, int n, int K) {
          (n & 7);
 }
 
-// Layout of the packed per-step metadata blob (device copy of ffmi_batch_desc).
+// Layout of the packed per-step metadata blob (device copy of ffmi_batch_desc):
+// [header 32 B][work items, 32 B each][tokens][commits].  The work array sits
+// at a FIXED offset, so a kernel's first two loads (header, its work item)
+// are independent instead of a dependent chain.
 struct BatchHeader {
   int32_t num_tokens, num_work, num_commits, num_mask_reqs;
   int32_t off_tokens, off_work, off_commits, off_masks;  // byte offsets
+};
+constexpr int kBlobWorkOffset = 32;
+static_assert(sizeof(BatchHeader) == kBlobWorkOffset, "work array follows the header");
+
+// Device work item: the ABI item plus what the host derives for the kernels.
+struct WorkDev {
+  ffmi_attn_work w;
+  int32_t clean;  // slots below this are not written by this step's commits
+                  // or stores for the item's request (loadable before them)
+  int32_t pad[3];
 };
 
 struct BatchView {
   const BatchHeader *hdr;
   const ffmi_token_info *tokens;
-  const ffmi_attn_work *work;
+  const WorkDev *work;
   const ffmi_commit_info *commits;
   const uint64_t *masks;
 };
@@ -59,8 +72,8 @@ struct BatchView {
 __device__ __forceinline__ BatchView batch_view(const char *blob) {
   BatchView v;
   v.hdr = reinterpret_cast<const BatchHeader *>(blob);
+  v.work = reinterpret_cast<const WorkDev *>(blob + kBlobWorkOffset);
   v.tokens = reinterpret_cast<const ffmi_token_info *>(blob + v.hdr->off_tokens);
-  v.work = reinterpret_cast<const ffmi_attn_work *>(blob + v.hdr->off_work);
   v.commits = reinterpret_cast<const ffmi_commit_info *>(blob + v.hdr->off_commits);
   v.masks = reinterpret_cast<const uint64_t *>(blob + v.hdr->off_masks);
   return v;
@@ -95,6 +108,7 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
                        Partials *defer = nullptr);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
+long attn_debug_stamps(long long *dst, long max_waves);
 long gemm_debug_stamps(long long *dst, long max_waves);
 size_t packed_act_bytes(int T, int K);
 hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s);

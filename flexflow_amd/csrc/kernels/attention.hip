@@ -28,10 +28,14 @@
 // out = sum(e_j v_j) / (sum_j e_j + 1e-6)   (inc...cu:532-547).
 //
 // Work decomposition: one workgroup per (work item = <=16 queries of one
-// request, head); its 4 waves stride over 32-key chunks with private online
+// request, head); its 8 waves stride over 32-key chunks with private online
 // softmax state and merge through LDS.  Every key/value byte of a request is
 // read once per 16-query tile (the reference's tree kernel re-reads the
 // whole K/V once per query, tree_inc...cu:135).
+#include <stdlib.h>
+
+#include <algorithm>
+
 #include "../ffmi_internal.h"
 
 namespace ffmi {
@@ -69,24 +73,158 @@ hipError_t launch_commit(const char *blob, int C, const uint16_t *stage, uint16_
 // Fused KV update of one step: RoPE (HF rotate-half, inc...cu:664-738) + KV
 // store (store_kv_cache inc...cu:35-61 / update_tree_branch_kv_cache_fused
 // tree_inc...cu:433-478 / spec_inc_store_kv_cache spec_inc...cu:311-358) +
-// staging copy for the next step's commits
-// for each (attention work item = <= 16 consecutive tokens of a request, head),
-// plus the TREE commits of the previous verify batch in extra blocks.
+// staging copy for the next step's commits, for one (attention work item =
+// <= NQ consecutive tokens of a request, head).  Shared by kv_update_kernel
+// and the FUSED attention prologue.
+//  * a thread unit is 4 consecutive rotation pairs (d = i0..i0+3 and
+//    i0+D/2..) of one token: 8-B fp16 or 16-B fp32-slab loads, 8-B stores;
+//  * every load of a thread (all its units, all slabs) is issued before its
+//    first store -- the update is a chain of dependent HBM round trips
+//    otherwise (units past q_count load token 0 and store nothing);
 //  * V goes through LDS so that V^T rows are written as runs of consecutive
-//    slots (16 lanes x 2 B) instead of one 2-byte store per (token, d);
-//  * commits read the OTHER half of the ping-pong staging (stage_rd) than the
-//    one this step writes (stage_wr), so both run in one launch.  The host
-//    launches commits separately first when a commit depth coincides with a
-//    slot this step stores (the reference's commit-then-store order).
+//    slots instead of one 2-byte store per (token, d).
+__device__ __forceinline__ f4 ld_h4(const uint16_t *p) {
+  const uint2 r = *reinterpret_cast<const uint2 *>(p);
+  return f4{h2f(r.x & 0xffff), h2f(r.x >> 16), h2f(r.y & 0xffff), h2f(r.y >> 16)};
+}
+__device__ __forceinline__ f4 round_h4(f4 a) {  // fp16 value of the combined sum
+  return f4{h2f(f2h(a[0])), h2f(f2h(a[1])), h2f(f2h(a[2])), h2f(f2h(a[3]))};
+}
+__device__ __forceinline__ void st_h4(uint16_t *p, uint16_t a, uint16_t b, uint16_t c,
+                                      uint16_t d) {
+  *reinterpret_cast<uint2 *>(p) = make_uint2(a | ((uint32_t)b << 16), c | ((uint32_t)d << 16));
+}
+
+template <int D, int NQ, int NT>
+__device__ __forceinline__ void kv_update_item(
+    const BatchView &bv, const ffmi_attn_work &w, int h, int heads, int slots, int T,
+    const uint16_t *__restrict__ qkv, const float *__restrict__ part, int pS, int pNP,
+    const float *__restrict__ rope, int max_rope_pos, uint16_t *__restrict__ qbuf,
+    uint16_t *__restrict__ kc, uint16_t *__restrict__ stage_wr, uint16_t (*sV)[NQ + 1],
+    int *sSlot, uint16_t (*sQ)[D + 8] = nullptr) {
+  constexpr int HD = D / 2, G = HD / 4, UNITS = NQ * G, U = (UNITS + NT - 1) / NT;
+  const int Hl = heads * D;
+  // channels: 0 q lo, 1 q hi, 2 k lo, 3 k hi, 4 v lo, 5 v hi
+  f4 x[U][6], cs[U][2];
+  ffmi_token_info ti[U];
+  int tl[U], i0[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = min((int)threadIdx.x + u * NT, UNITS - 1);
+    tl[u] = e / G, i0[u] = (e % G) * 4;
+    const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
+    ti[u] = bv.tokens[t];
+    const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
+                        Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
+                        2 * Hl + h * D + i0[u] + HD};
+    if (part) {
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        x[u][c] = *reinterpret_cast<const f4 *>(part + (size_t)t * pNP + col[c]);
+    } else {
+#pragma unroll
+      for (int c = 0; c < 6; ++c) x[u][c] = ld_h4(qkv + (size_t)t * 3 * Hl + col[c]);
+    }
+  }
+  if (part) {  // remaining slabs in slice order, then fp16 (partials_value)
+    const size_t slab = (size_t)T * pNP;
+    for (int sl = 1; sl < pS; ++sl)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
+        const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
+                            Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
+                            2 * Hl + h * D + i0[u] + HD};
+#pragma unroll
+        for (int c = 0; c < 6; ++c)
+          x[u][c] += *reinterpret_cast<const f4 *>(part + sl * slab + (size_t)t * pNP + col[c]);
+      }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) x[u][c] = round_h4(x[u][c]);
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int pos = min(max(ti[u].pos, 0), max_rope_pos - 1);
+    const f4 *r = reinterpret_cast<const f4 *>(rope + ((size_t)pos * HD + i0[u]) * 2);
+    cs[u][0] = r[0];  // c0 s0 c1 s1
+    cs[u][1] = r[1];  // c2 s2 c3 s3
+  }
+  // ---- stores
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (tl[u] >= w.q_count || (int)threadIdx.x + u * NT >= UNITS) continue;
+    const int t = w.q_start + tl[u];
+    uint16_t qlo[4], qhi[4], klo[4], khi[4], vlo[4], vhi[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float c = cs[u][j >> 1][(j & 1) * 2], sn = cs[u][j >> 1][(j & 1) * 2 + 1];
+      const float qa = x[u][0][j], qb = x[u][1][j], ka = x[u][2][j], kb = x[u][3][j];
+      qlo[j] = f2h(__fsub_rn(__fmul_rn(qa, c), __fmul_rn(qb, sn)));
+      qhi[j] = f2h(__fadd_rn(__fmul_rn(qa, sn), __fmul_rn(qb, c)));
+      klo[j] = f2h(__fsub_rn(__fmul_rn(ka, c), __fmul_rn(kb, sn)));
+      khi[j] = f2h(__fadd_rn(__fmul_rn(ka, sn), __fmul_rn(kb, c)));
+      vlo[j] = f2h(x[u][4][j]);
+      vhi[j] = f2h(x[u][5][j]);
+    }
+    // rotated q: to LDS for the same workgroup's attention (fused), else HBM
+    uint16_t *qo = sQ ? &sQ[tl[u]][i0[u]] : qbuf + (size_t)t * Hl + h * D + i0[u];
+    st_h4(qo, qlo[0], qlo[1], qlo[2], qlo[3]);
+    st_h4(qo + HD, qhi[0], qhi[1], qhi[2], qhi[3]);
+    const bool store = ti[u].store_slot >= 0 && ti[u].store_slot < slots;
+    if (store) {
+      uint16_t *kr = kc + (((size_t)ti[u].req * heads + h) * slots + ti[u].store_slot) * D + i0[u];
+      st_h4(kr, klo[0], klo[1], klo[2], klo[3]);
+      st_h4(kr + HD, khi[0], khi[1], khi[2], khi[3]);
+    }
+    if (i0[u] == 0) sSlot[tl[u]] = store ? ti[u].store_slot : -1;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      sV[i0[u] + j][tl[u]] = vlo[j];
+      sV[i0[u] + HD + j][tl[u]] = vhi[j];
+    }
+    if (stage_wr) {
+      uint16_t *st = stage_wr + (size_t)t * 2 * Hl + h * D + i0[u];
+      st_h4(st, klo[0], klo[1], klo[2], klo[3]);
+      st_h4(st + HD, khi[0], khi[1], khi[2], khi[3]);
+      st_h4(st + Hl, vlo[0], vlo[1], vlo[2], vlo[3]);
+      st_h4(st + Hl + HD, vhi[0], vhi[1], vhi[2], vhi[3]);
+    }
+  }
+}
+
+// V^T[req][h][d][slot] rows from the LDS tile: lanes run over consecutive
+// tokens of a d-row (call after a barrier that follows kv_update_item)
+template <int D, int NQ>
+__device__ __forceinline__ void kv_store_vt(const ffmi_attn_work &w, int h, int heads, int slots,
+                                            uint16_t *__restrict__ vc,
+                                            const uint16_t (*sV)[NQ + 1], const int *sSlot) {
+  uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
+  for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
+    const int dd = e / NQ, tt = e % NQ;
+    if (tt >= w.q_count) continue;
+    const int sl = sSlot[tt];
+    if (sl >= 0) vt[(size_t)dd * slots + sl] = sV[dd][tt];
+  }
+}
+
+// Standalone KV update (items with more tokens than one attention launch
+// should carry in its prologue): one workgroup per (item, head), one thread
+// per unit, plus the TREE commits of the previous verify batch in extra
+// blocks.  Commits read the OTHER half of the ping-pong staging (stage_rd)
+// than the one this step writes (stage_wr), so both run in one launch; the
+// host launches commits separately first when a commit depth coincides with
+// a slot this step stores (the reference's commit-then-store order).
 template <int D>
-__global__ __launch_bounds__(16 * D / 2) void kv_update_kernel(
+__global__ __launch_bounds__(FFMI_ATTN_QTILE * D / 8) void kv_update_kernel(
     const char *__restrict__ blob, int T, int W, int C, const uint16_t *__restrict__ qkv,
     const float *__restrict__ part, int pS, int pNP, uint16_t *__restrict__ qbuf,
     uint16_t *__restrict__ kc, uint16_t *__restrict__ vc, uint16_t *__restrict__ stage_wr,
     const uint16_t *__restrict__ stage_rd, const float *__restrict__ rope, int heads, int slots,
     int max_rope_pos) {
-  constexpr int HD = D / 2;  // one thread per (token of a 16-token half, rotation pair)
   constexpr int NQ = FFMI_ATTN_QTILE;
+  constexpr int NT = NQ * D / 8;
   __shared__ uint16_t sV[D][NQ + 1];
   __shared__ int sSlot[NQ];
   const int Hl = heads * D;
@@ -105,57 +243,11 @@ __global__ __launch_bounds__(16 * D / 2) void kv_update_kernel(
     }
     return;
   }
-  const ffmi_attn_work w = bv.work[item];
-  const int i = threadIdx.x % HD;
-  for (int tl = threadIdx.x / HD; tl < NQ; tl += 16) {
-    if (tl >= w.q_count) break;
-    const int t = w.q_start + tl;
-    const ffmi_token_info ti = bv.tokens[t];
-    auto qkv_at = [&](int col) -> float {
-      return part ? partials_value(part, pS, pNP, T, t, col)
-                  : h2f(qkv[(size_t)t * 3 * Hl + col]);
-    };
-    const int qc = h * D, kc0 = Hl + h * D, vc0 = 2 * Hl + h * D;
-    const float qa = qkv_at(qc + i), qb = qkv_at(qc + i + HD);
-    const float ka = qkv_at(kc0 + i), kb = qkv_at(kc0 + i + HD);
-    const float va = qkv_at(vc0 + i), vb = qkv_at(vc0 + i + HD);
-    const int pos = min(max(ti.pos, 0), max_rope_pos - 1);
-    const float c = rope[((size_t)pos * HD + i) * 2 + 0];
-    const float s = rope[((size_t)pos * HD + i) * 2 + 1];
-    const uint16_t q0 = f2h(__fsub_rn(__fmul_rn(qa, c), __fmul_rn(qb, s)));
-    const uint16_t q1 = f2h(__fadd_rn(__fmul_rn(qa, s), __fmul_rn(qb, c)));
-    const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(ka, c), __fmul_rn(kb, s)));
-    const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(ka, s), __fmul_rn(kb, c)));
-    const uint16_t v0 = f2h(va), v1 = f2h(vb);
-    uint16_t *qo = qbuf + (size_t)t * Hl + h * D;
-    qo[i] = q0;
-    qo[i + HD] = q1;
-    const bool store = ti.store_slot >= 0 && ti.store_slot < slots;
-    if (store) {
-      uint16_t *kr = kc + (((size_t)ti.req * heads + h) * slots + ti.store_slot) * D;
-      kr[i] = k0;
-      kr[i + HD] = k1;
-    }
-    if (i == 0) sSlot[tl] = store ? ti.store_slot : -1;
-    sV[i][tl] = v0;
-    sV[i + HD][tl] = v1;
-    if (stage_wr) {
-      uint16_t *st = stage_wr + (size_t)t * 2 * Hl + h * D;
-      st[i] = k0;
-      st[i + HD] = k1;
-      st[Hl + i] = v0;
-      st[Hl + i + HD] = v1;
-    }
-  }
+  const ffmi_attn_work w = bv.work[item].w;
+  kv_update_item<D, NQ, NT>(bv, w, h, heads, slots, T, qkv, part, pS, pNP, rope, max_rope_pos,
+                            qbuf, kc, stage_wr, sV, sSlot);
   __syncthreads();
-  // ---- V^T[req][h][d][slot]: lanes run over consecutive tokens of a d-row
-  uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
-  for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
-    const int dd = e / NQ, tt = e % NQ;
-    if (tt >= w.q_count) continue;
-    const int sl = sSlot[tt];
-    if (sl >= 0) vt[(size_t)dd * slots + sl] = sV[dd][tt];
-  }
+  kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
 }
 
 hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_t *qkv,
@@ -166,11 +258,11 @@ hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_
   const dim3 grid((W + C) * heads);
   const float *pp = qkvp.S > 0 ? qkvp.p : nullptr;
   if (d == 128)
-    hipLaunchKernelGGL(kv_update_kernel<128>, grid, dim3(1024), 0, s, blob, T, W, C, qkv, pp,
+    hipLaunchKernelGGL(kv_update_kernel<128>, grid, dim3(FFMI_ATTN_QTILE * 16), 0, s, blob, T, W, C, qkv, pp,
                        qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
                        max_rope_pos);
   else if (d == 64)
-    hipLaunchKernelGGL(kv_update_kernel<64>, grid, dim3(512), 0, s, blob, T, W, C, qkv, pp,
+    hipLaunchKernelGGL(kv_update_kernel<64>, grid, dim3(FFMI_ATTN_QTILE * 8), 0, s, blob, T, W, C, qkv, pp,
                        qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
                        max_rope_pos);
   else
@@ -181,9 +273,9 @@ hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_
 // visibility from registers only: prefix range + the query's 64-bit tree word
 __device__ __forceinline__ bool key_visible(int slot, int prefix_len, int tree_base,
                                             int tree_len, uint64_t tree_vis) {
-  if (slot < prefix_len) return true;
   const unsigned j = (unsigned)(slot - tree_base);
-  return j < (unsigned)tree_len && ((tree_vis >> j) & 1ull);
+  const bool in_tree = j < (unsigned)tree_len && ((tree_vis >> (j & 63)) & 1ull);
+  return (slot < prefix_len) | in_tree;  // no branches: one select per key
 }
 
 // Arguments of the fused prologue (FUSED kernels only; see attention_kernel).
@@ -196,10 +288,12 @@ struct KvUpdateArgs {
   const uint16_t *stage_rd;
   const float *rope;
   int max_rope_pos;
+  long long *stamps;  // ST kernels: per-wave timeline (diagnostics)
 };
 
 // One workgroup per (work item = <= 16*QT consecutive queries of a request,
-// head); 4 waves stride over 32-key chunks with private online-softmax state
+// head); NW = 8 waves (two per SIMD: each hides the other's load latency)
+// stride over 32-key chunks with private online-softmax state
 // and merge through LDS.  QT query tiles share every K / V^T fragment load.
 //
 // FUSED (host-checked: each request has exactly one work item this step, as
@@ -207,96 +301,91 @@ struct KvUpdateArgs {
 // own request's TREE commits and the KV update of its own tokens for its
 // head (kv_update_kernel's work), makes them visible to the workgroup, then
 // attends -- one launch per step instead of two.
-template <int D, int QT, bool FUSED>
-__global__ __launch_bounds__(256, 2) void attention_kernel(
+template <int D, int QT, int NW, bool FUSED, bool ST = false>
+__global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     const char *__restrict__ blob, uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
     uint16_t *__restrict__ vc, uint16_t *__restrict__ out, int heads, int slots, float scale,
     int out_packed, KvUpdateArgs kv) {
   constexpr int KS = D / 32;  // k-steps of the QK^T product
   constexpr int DT = D / 16;  // d-tiles of the PV product
   constexpr int NQ = 16 * QT;
-  __shared__ float sm_m[4][NQ];
-  __shared__ float sm_l[4][NQ];
-  __shared__ __attribute__((aligned(16))) float sm_o[4][QT][DT][4][64];
+  __shared__ float sm_m[NW][NQ];
+  __shared__ float sm_l[NW][NQ];
+  __shared__ __attribute__((aligned(16))) float sm_o[NW][QT][DT][4][64];
 
+  long long st[6] = {0, 0, 0, 0, 0, 0};
+  if (ST) st[0] = __builtin_amdgcn_s_memrealtime();
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int qi = lane & 15;
   const int g = lane >> 4;
   const int h = blockIdx.y;
   const BatchView bv = batch_view(blob);
-  const ffmi_attn_work w = bv.work[blockIdx.x];
+  const WorkDev wd = bv.work[blockIdx.x];
+  const ffmi_attn_work w = wd.w;
   const int Hl = heads * D;
+  const uint16_t *kbase = kc + ((size_t)w.req * heads + h) * slots * D;
+  const uint16_t *vbase = vc + ((size_t)w.req * heads + h) * D * slots;
+  // K rows and V^T columns of one 32-key chunk (chunk indices are clamped by
+  // the caller: the cache is allocated to a multiple of 32 slots)
+  auto load_chunk = [&](int c, h8 (&kf)[2][KS], h8 (&va)[DT]) {
+    const int base = c * 32;
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const uint16_t *krow = kbase + (size_t)(base + sub * 16 + (lane & 15)) * D + 8 * g;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[sub][ks] = *reinterpret_cast<const h8 *>(krow + 32 * ks);
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t *vrow = vbase + (size_t)(t * 16 + (lane & 15)) * slots + base + 4 * g;
+      h4 v0 = *reinterpret_cast<const h4 *>(vrow);
+      h4 v1 = *reinterpret_cast<const h4 *>(vrow + 16);
+      va[t] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+  };
+  // FUSED: a wave's first chunk lies below every slot this step writes for
+  // the request (host-computed `clean`): its loads go out before the
+  // KV-update prologue and land while the prologue runs
+  const int nchunks = (w.kv_len + 31) >> 5;
+  h8 kf0[2][KS], va0[DT];
+  const bool early = FUSED && wave < nchunks && (wave + 1) * 32 <= wd.clean;
+  if (early) load_chunk(wave, kf0, va0);
 
+  // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
   if (FUSED) {
-    constexpr int HD = D / 2;
     __shared__ uint16_t sV[D][NQ + 1];
     __shared__ int sSlot[NQ];
-    // (1) commits of this request (commit before store, as the reference)
-    for (int e = threadIdx.x; e < kv.C * D; e += blockDim.x) {
-      const ffmi_commit_info cm = bv.commits[e / D];
-      const int i = e % D;
+    // (1) commits of this request (the host launches them separately when a
+    // commit depth coincides with a slot stored below), 16-B rows
+    constexpr int D8 = D / 8;
+    for (int e = threadIdx.x; e < kv.C * D8; e += blockDim.x) {
+      const ffmi_commit_info cm = bv.commits[e / D8];
+      const int i = (e % D8) * 8;
       if (cm.req != w.req || cm.depth < 0 || cm.depth >= slots) continue;
-      const uint16_t *st = kv.stage_rd + (size_t)cm.src_token * 2 * Hl + h * D;
-      kc[(((size_t)cm.req * heads + h) * slots + cm.depth) * D + i] = st[i];
-      vc[(((size_t)cm.req * heads + h) * D + i) * slots + cm.depth] = st[Hl + i];
+      const uint16_t *st = kv.stage_rd + (size_t)cm.src_token * 2 * Hl + h * D + i;
+      const uint4 kk = *reinterpret_cast<const uint4 *>(st);
+      const uint4 vv = *reinterpret_cast<const uint4 *>(st + Hl);
+      *reinterpret_cast<uint4 *>(kc + (((size_t)cm.req * heads + h) * slots + cm.depth) * D + i) = kk;
+      uint16_t *vt = vc + (((size_t)cm.req * heads + h) * D + i) * slots + cm.depth;
+      const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+      for (int j = 0; j < 8; ++j) vt[(size_t)j * slots] = (uint16_t)(vw[j >> 1] >> (16 * (j & 1)));
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
     // (2) RoPE + KV store + staging of this item's tokens, this head
-    for (int e = threadIdx.x; e < NQ * HD; e += blockDim.x) {
-      const int tl = e / HD, i = e % HD;
-      if (tl >= w.q_count) continue;
-      const int t = w.q_start + tl;
-      const ffmi_token_info ti = bv.tokens[t];
-      auto qkv_at = [&](int col) -> float {
-        return kv.part ? partials_value(kv.part, kv.pS, kv.pNP, kv.T, t, col)
-                       : h2f(kv.qkv[(size_t)t * 3 * Hl + col]);
-      };
-      const int qc = h * D, kc0 = Hl + h * D, vc0 = 2 * Hl + h * D;
-      const float qa = qkv_at(qc + i), qb = qkv_at(qc + i + HD);
-      const float ka = qkv_at(kc0 + i), kb = qkv_at(kc0 + i + HD);
-      const float va = qkv_at(vc0 + i), vb = qkv_at(vc0 + i + HD);
-      const int pos = min(max(ti.pos, 0), kv.max_rope_pos - 1);
-      const float c = kv.rope[((size_t)pos * HD + i) * 2 + 0];
-      const float sn = kv.rope[((size_t)pos * HD + i) * 2 + 1];
-      const uint16_t k0 = f2h(__fsub_rn(__fmul_rn(ka, c), __fmul_rn(kb, sn)));
-      const uint16_t k1 = f2h(__fadd_rn(__fmul_rn(ka, sn), __fmul_rn(kb, c)));
-      const uint16_t v0 = f2h(va), v1 = f2h(vb);
-      uint16_t *qo = qbuf + (size_t)t * Hl + h * D;
-      qo[i] = f2h(__fsub_rn(__fmul_rn(qa, c), __fmul_rn(qb, sn)));
-      qo[i + HD] = f2h(__fadd_rn(__fmul_rn(qa, sn), __fmul_rn(qb, c)));
-      const bool store = ti.store_slot >= 0 && ti.store_slot < slots;
-      if (store) {
-        uint16_t *kr = kc + (((size_t)ti.req * heads + h) * slots + ti.store_slot) * D;
-        kr[i] = k0;
-        kr[i + HD] = k1;
-      }
-      if (i == 0) sSlot[tl] = store ? ti.store_slot : -1;
-      sV[i][tl] = v0;
-      sV[i + HD][tl] = v1;
-      if (kv.stage_wr) {
-        uint16_t *st = kv.stage_wr + (size_t)t * 2 * Hl + h * D;
-        st[i] = k0;
-        st[i + HD] = k1;
-        st[Hl + i] = v0;
-        st[Hl + i + HD] = v1;
-      }
-    }
+    kv_update_item<D, NQ, 64 * NW>(bv, w, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP,
+                               kv.rope, kv.max_rope_pos, qbuf, kc, kv.stage_wr, sV, sSlot,
+                               sQ);
     __syncthreads();
-    uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
-    for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
-      const int dd = e / NQ, tt = e % NQ;
-      if (tt >= w.q_count) continue;
-      const int sl = sSlot[tt];
-      if (sl >= 0) vt[(size_t)dd * slots + sl] = sV[dd][tt];
-    }
+    kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
     // this workgroup's stores become visible to its own loads below (the
     // (req, head) K/V lines are touched by no other workgroup this step)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
+  if (ST) st[1] = __builtin_amdgcn_s_memrealtime();
   bool qvalid[QT];
   int pre[QT], tb[QT], tlen[QT];
   uint64_t tv[QT];
@@ -309,12 +398,11 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
     pre[qt] = ti.prefix_len, tb[qt] = ti.tree_base, tlen[qt] = ti.tree_len, tv[qt] = ti.tree_vis;
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
-      qf[qt][ks] = qvalid[qt] ? *reinterpret_cast<const h8 *>(
-                                    qbuf + (size_t)(w.q_start + q) * Hl + h * D + 32 * ks + 8 * g)
-                              : h8{0, 0, 0, 0, 0, 0, 0, 0};
+      qf[qt][ks] = !qvalid[qt] ? h8{0, 0, 0, 0, 0, 0, 0, 0}
+                   : FUSED ? *reinterpret_cast<const h8 *>(&sQ[q][32 * ks + 8 * g])
+                           : *reinterpret_cast<const h8 *>(
+                                 qbuf + (size_t)(w.q_start + q) * Hl + h * D + 32 * ks + 8 * g);
   }
-  const uint16_t *kbase = kc + ((size_t)w.req * heads + h) * slots * D;
-  const uint16_t *vbase = vc + ((size_t)w.req * heads + h) * D * slots;
 
   const float NEG = -INFINITY;
   float m_run[QT], l_run[QT];
@@ -326,25 +414,7 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
     for (int t = 0; t < DT; ++t) o[qt][t] = f4{0.f, 0.f, 0.f, 0.f};
   }
 
-  const int nchunks = (w.kv_len + 31) >> 5;
-  for (int c = wave; c < nchunks; c += 4) {
-    const int base = c * 32;
-    h8 kf[2][KS];
-#pragma unroll
-    for (int sub = 0; sub < 2; ++sub) {
-      const uint16_t *krow = kbase + (size_t)(base + sub * 16 + (lane & 15)) * D + 8 * g;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) kf[sub][ks] = *reinterpret_cast<const h8 *>(krow + 32 * ks);
-    }
-    // V^T fragments for this chunk (issued early; consumed after softmax)
-    h8 va[DT];
-#pragma unroll
-    for (int t = 0; t < DT; ++t) {
-      const uint16_t *vrow = vbase + (size_t)(t * 16 + (lane & 15)) * slots + base + 4 * g;
-      h4 v0 = *reinterpret_cast<const h4 *>(vrow);
-      h4 v1 = *reinterpret_cast<const h4 *>(vrow + 16);
-      va[t] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
-    }
+  auto compute_chunk = [&](int base, const h8 (&kf)[2][KS], const h8 (&va)[DT]) {
 #pragma unroll
     for (int qt = 0; qt < QT; ++qt) {
       // S^T = K . Q^T: this lane holds query qt*16+qi, keys base + 16 sub + 4 g + r
@@ -391,8 +461,21 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
         o[qt][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(va[t], plo, o[qt][t], 0, 0, 0);
       }
     }
+  };
+  // wave w takes chunks w, w+NW, ... (two waves per SIMD hide each other's
+  // load latency; per-wave double buffering would not fit the registers)
+  if (ST) st[2] = __builtin_amdgcn_s_memrealtime();
+  for (int c = wave; c < nchunks; c += NW) {
+    if (early && c == wave) {
+      compute_chunk(c * 32, kf0, va0);
+      continue;
+    }
+    h8 kf[2][KS], va[DT];
+    load_chunk(c, kf, va);
+    compute_chunk(c * 32, kf, va);
   }
 
+  if (ST) st[3] = __builtin_amdgcn_s_memrealtime();
   // per-query partial sum over the 4 lane groups (same m_run in all four)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -409,17 +492,18 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
       for (int r = 0; r < 4; ++r) sm_o[wave][qt][t][r][lane] = o[qt][t][r];
   }
   __syncthreads();
+  if (ST) st[4] = __builtin_amdgcn_s_memrealtime();
 
-  // merge: wave w finalizes d-tiles t = w, w+4, ... of every query tile
+  // merge: wave w finalizes d-tiles t = w, w+NW, ... of every query tile
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
     const int q = qt * 16 + qi;
     float M = NEG;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_m[ww][q]);
-    float f[4], L = 0.f;
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, sm_m[ww][q]);
+    float f[NW], L = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < 4; ++ww) {
+    for (int ww = 0; ww < NW; ++ww) {
       const float mw = sm_m[ww][q];
       f[ww] = (mw == NEG) ? 0.f : __expf(mw - M);
       L += f[ww] * sm_l[ww][q];
@@ -428,13 +512,13 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
     if (!qvalid[qt]) continue;
     const int orow_m = w.q_start + q;
     uint16_t *orow = out + (size_t)orow_m * Hl + h * D;
-    for (int t = wave; t < DT; t += 4) {
+    for (int t = wave; t < DT; t += NW) {
       uint16_t r4[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         float acc = 0.f;
 #pragma unroll
-        for (int ww = 0; ww < 4; ++ww) acc += f[ww] * sm_o[ww][qt][t][r][lane];
+        for (int ww = 0; ww < NW; ++ww) acc += f[ww] * sm_o[ww][qt][t][r][lane];
         r4[r] = f2h(acc * inv);
       }
       uint2 pk;
@@ -443,6 +527,18 @@ __global__ __launch_bounds__(256, 2) void attention_kernel(
       uint16_t *dst = out_packed ? out + act_packed_off(orow_m, h * D + t * 16 + 4 * g, Hl)
                                  : orow + t * 16 + 4 * g;
       *reinterpret_cast<uint2 *>(dst) = pk;
+    }
+  }
+  if (ST && kv.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    st[5] = __builtin_amdgcn_s_memrealtime();
+    unsigned hwid;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
+    if (lane == 0) {
+      long long *d = kv.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + wave) * 8;
+      for (int i = 0; i < 6; ++i) d[i] = st[i];
+      d[6] = hwid;
+      d[7] = nchunks;
     }
   }
 }
@@ -454,8 +550,17 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
                                      const KvUpdateArgs &kv) {
   const dim3 grid(W, heads);
 #define FFMI_ATT(QT, FU)                                                                     \
-  hipLaunchKernelGGL((attention_kernel<D, QT, FU>), grid, dim3(256), 0, s, blob, qbuf, kc, vc, \
-                     out, heads, slots, scale, op, kv)
+  hipLaunchKernelGGL((attention_kernel<D, QT, 8, FU>), grid, dim3(512), 0, s, blob, qbuf, kc,  \
+                     vc, out, heads, slots, scale, op, kv)
+  if (kv.stamps && D == 128 && max_q > 16) {  // diagnostics build of the verify kernels
+    if (fused)
+      hipLaunchKernelGGL((attention_kernel<D, 2, 8, true, true>), grid, dim3(512), 0, s, blob,
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv);
+    else
+      hipLaunchKernelGGL((attention_kernel<D, 2, 8, false, true>), grid, dim3(512), 0, s, blob,
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv);
+    return hipGetLastError();
+  }
   if (max_q <= 16) {
     if (fused) FFMI_ATT(1, true);
     else FFMI_ATT(1, false);
@@ -465,6 +570,27 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
   }
 #undef FFMI_ATT
   return hipGetLastError();
+}
+
+// FFMI_ATTN_STAMP=1: verify-size launches record a per-wave timeline
+// {start, after prologue, before k-loop, after k-loop, after merge barrier,
+// end, HW_ID, chunks} (100 MHz realtime) for ffmi_debug_attn_stamps.
+static long long *g_attn_stamps = nullptr;
+static long g_attn_stamp_waves = 0;
+static long long *attn_stamp_buf(int wgs) {
+  static const bool on = getenv("FFMI_ATTN_STAMP") != nullptr;
+  if (!on) return nullptr;
+  if (!g_attn_stamps && hipMalloc(&g_attn_stamps, (size_t)8 << 20) != hipSuccess) return nullptr;
+  g_attn_stamp_waves = std::min<long>((long)wgs * 8, ((long)8 << 20) / 64);
+  return g_attn_stamps;
+}
+
+long attn_debug_stamps(long long *dst, long max_waves) {
+  if (!g_attn_stamps || max_waves <= 0) return 0;
+  const long n = std::min(max_waves, g_attn_stamp_waves);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(dst, g_attn_stamps, (size_t)n * 64, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
 }
 
 // fused == false: the KV of this step must already be in the cache
@@ -478,8 +604,9 @@ hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, 
   if (W <= 0) return hipSuccess;
   if (out_packed && (heads * d) % 32) return hipErrorInvalidValue;
   if (max_q > FFMI_ATTN_QTILE) return hipErrorInvalidValue;
-  const KvUpdateArgs kv{T, C, qkv, qkvp.S > 0 ? qkvp.p : nullptr, qkvp.S, qkvp.NP,
-                        stage_wr, stage_rd, rope, max_rope_pos};
+  const KvUpdateArgs kv{T,        C,        qkv,  qkvp.S > 0 ? qkvp.p : nullptr,
+                        qkvp.S,   qkvp.NP,  stage_wr, stage_rd,
+                        rope,     max_rope_pos, attn_stamp_buf(W * heads)};
   const int op = out_packed ? 1 : 0;
   if (d == 128)
     return launch_attention_d<128>(blob, W, max_q, qbuf, kc, vc, out, heads, slots, scale, s, op,

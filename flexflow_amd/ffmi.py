@@ -155,6 +155,7 @@ SIGNATURES = {
                                 c_float, c_int, c_void_p]),
     "ffmi_pack_activations": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_debug_gemm_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
+    "ffmi_debug_attn_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
 }
 
 _lib = None

@@ -428,6 +428,43 @@ def test_attention_tree_verify_and_commit(d):
         close16(out[j], c.ref_row(qs[j], 1, vis), exact_frac=0.98)
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_attention_tree_fused_equals_two_launch_path(d, monkeypatch):
+    """Verify steps (21-token trees for two requests, commits of the previous
+    step) through the one-launch path and the KV-update + attention path:
+    outputs, K cache and V^T cache bit-identical."""
+    def scenario():
+        rng = np.random.default_rng(300 + d)
+        c = AttnCase(F.ATTN_TREE, d=d)
+        infos = [(3, p, r, p, p + 1, 0, 0, 0) for r in (0, 2) for p in range(12)]
+        o1, _ = c.run(infos, masks=[[0]] * 3, rng=rng)
+        parents = [-1, 0, 1] + [2 + (j - 3) // 3 for j in range(3, 21)]
+        m = tree_masks(parents)
+        depth = [12]
+        for j in range(1, 21):
+            depth.append(depth[parents[j]] + 1)
+        infos = [(4, depth[j], r, 12 + j, 12, 12, 21, j) for r in (0, 2) for j in range(21)]
+        o2, _ = c.run(infos, masks=[m, [0], m], rng=rng)
+        # accept a path of 4 per request, then a fresh 21-token tree at 16
+        commits = [(21 * k + j, r, 12 + i) for k, r in enumerate((0, 2))
+                   for i, j in enumerate([0, 1, 2, 5])]
+        infos = [(4, depth[j] + 4, r, 16 + j, 16, 16, 21, j) for r in (0, 2) for j in range(21)]
+        o3, _ = c.run(infos, masks=[m, [0], m], commits=commits, rng=rng)
+        k, v = ctypes.c_void_p(), ctypes.c_void_p()
+        slots = ctypes.c_int()
+        F.check(L.ffmi_attn_kv_ptrs(c.h, ctypes.byref(k), ctypes.byref(v), ctypes.byref(slots)))
+        n = 4 * c.heads * slots.value * c.d
+        kc, vc = np.empty(n, np.uint16), np.empty(n, np.uint16)
+        hip().hipMemcpy(kc.ctypes.data, k, n * 2, 2)
+        hip().hipMemcpy(vc.ctypes.data, v, n * 2, 2)
+        return o1, o2, o3, kc, vc
+    fused = scenario()
+    monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
+    split = scenario()
+    for a, b in zip(fused, split):
+        assert np.array_equal(np.asarray(a).view(np.uint16), np.asarray(b).view(np.uint16))
+
+
 def test_attention_spec_beam_layers():
     rng = np.random.default_rng(7)
     c = AttnCase(F.ATTN_SPEC, d=64)
