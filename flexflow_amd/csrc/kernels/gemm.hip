@@ -287,6 +287,8 @@ __device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *_
       for (int i = 0; i < MTW; ++i) {
         const int m = m0 + i * 16 + mr;
         if (m < T)
+          // (non-temporal stores here measured slower end to end: the
+          // consumer then reads the slabs from memory instead of L2)
           *reinterpret_cast<f4 *>(Ypart + ((size_t)ks * T + m) * NP + tile * 16 + nq) = acc[i][j];
       }
     }
@@ -536,13 +538,23 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
     }
   }
-  // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split
+  // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split of
+  // every M-split launch; "N:K:NTW,S;..." only of the listed shapes
   static const char *force = getenv("FFMI_GEMM_PLAN");
   if (force) {
-    int ntw = 0, S = 0;
-    if (sscanf(force, "%d,%d", &ntw, &S) == 2 && (ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) &&
-        S >= 1 && S <= KT)
-      p.NTW = ntw, p.S = S;
+    const char *q = force;
+    while (q && *q) {
+      int a = 0, b = 0, c = 0, d = 0, ntw = 0, S = 0;
+      const int n = sscanf(q, "%d:%d:%d,%d", &a, &b, &c, &d);
+      if (n == 4 && a == N && b == K) ntw = c, S = d;
+      else if (n != 4 && sscanf(q, "%d,%d", &a, &b) == 2) ntw = a, S = b;
+      if ((ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) && S >= 1 && S <= KT) {
+        p.NTW = ntw, p.S = S;
+        break;
+      }
+      q = strchr(q, ';');
+      if (q) ++q;
+    }
   }
   p.nblk = (ntiles + p.NTW - 1) / p.NTW;
   return p;
