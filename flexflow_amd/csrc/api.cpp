@@ -112,6 +112,12 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
         if (d->commits[c].req == x.w.req && d->commits[c].depth >= 0)
           clean = std::min(clean, (int)d->commits[c].depth);
       x.clean = clean;
+      for (int j = 0; j < FFMI_ATTN_QTILE; ++j) {
+        const int t = x.w.q_start + std::min(j, std::max(x.w.q_count - 1, 0));
+        const int pos = t < d->num_tokens ? d->tokens[t].pos : 0;
+        // the kernels clamp to their table (rows = cache slots <= 32768)
+        x.rope_pos[j] = (int16_t)std::min(std::max(pos, 0), 32767);
+      }
       wd[wi] = x;
     }
   }

@@ -59,7 +59,12 @@ struct WorkDev {
   int32_t clean;  // slots below this are not written by this step's commits
                   // or stores for the item's request (loadable before them)
   int32_t pad[3];
+  // RoPE position of each of the item's tokens (clamped to [0, 32767]; the
+  // kernels clamp to their table): the table loads then depend on the work
+  // item only, not on the token records
+  int16_t rope_pos[FFMI_ATTN_QTILE];
 };
+static_assert(sizeof(WorkDev) % 16 == 0, "16-B aligned work items");
 
 struct BatchView {
   const BatchHeader *hdr;

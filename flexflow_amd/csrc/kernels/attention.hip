@@ -95,40 +95,59 @@ __device__ __forceinline__ void st_h4(uint16_t *p, uint16_t a, uint16_t b, uint1
   *reinterpret_cast<uint2 *>(p) = make_uint2(a | ((uint32_t)b << 16), c | ((uint32_t)d << 16));
 }
 
-template <int D, int NQ, int NT>
+// after_loads() runs once this thread's update loads are in flight (the
+// fused attention issues its first K/V chunk there: loads complete in issue
+// order, so anything issued BEFORE these would delay them).
+template <int D, int NQ, int NT, class AfterLoads>
 __device__ __forceinline__ void kv_update_item(
-    const BatchView &bv, const ffmi_attn_work &w, int h, int heads, int slots, int T,
+    const BatchView &bv, const WorkDev *__restrict__ wdp, int h, int heads, int slots, int T,
     const uint16_t *__restrict__ qkv, const float *__restrict__ part, int pS, int pNP,
     const float *__restrict__ rope, int max_rope_pos, uint16_t *__restrict__ qbuf,
     uint16_t *__restrict__ kc, uint16_t *__restrict__ stage_wr, uint16_t (*sV)[NQ + 1],
-    int *sSlot, uint16_t (*sQ)[D + 8] = nullptr) {
+    int *sSlot, uint16_t (*sQ)[D + 8], AfterLoads &&after_loads) {
   constexpr int HD = D / 2, G = HD / 4, UNITS = NQ * G, U = (UNITS + NT - 1) / NT;
   const int Hl = heads * D;
+  const ffmi_attn_work w = wdp->w;
   // channels: 0 q lo, 1 q hi, 2 k lo, 3 k hi, 4 v lo, 5 v hi
-  f4 x[U][6], cs[U][2];
-  ffmi_token_info ti[U];
+  f4 x[U][6], y[U][6], cs[U][2];  // y: second fp32 slab
+  int tslot[U], treq[U];  // (scalar fields: a struct copy would go to scratch)
   int tl[U], i0[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int e = min((int)threadIdx.x + u * NT, UNITS - 1);
     tl[u] = e / G, i0[u] = (e % G) * 4;
     const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
-    ti[u] = bv.tokens[t];
+    tslot[u] = bv.tokens[t].store_slot;
+    treq[u] = bv.tokens[t].req;
+    const int pos = min((int)wdp->rope_pos[tl[u] < w.q_count ? tl[u] : 0], max_rope_pos - 1);
+    const f4 *r = reinterpret_cast<const f4 *>(rope + ((size_t)pos * HD + i0[u]) * 2);
+    cs[u][0] = r[0];  // c0 s0 c1 s1
+    cs[u][1] = r[1];  // c2 s2 c3 s3
     const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
                         Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
                         2 * Hl + h * D + i0[u] + HD};
-    if (part) {
+    if (part) {  // slabs 0 and 1 (slab 0 again when pS == 1: no branch)
+      const float *p1 = part + (pS > 1 ? (size_t)T * pNP : 0);
 #pragma unroll
       for (int c = 0; c < 6; ++c)
         x[u][c] = *reinterpret_cast<const f4 *>(part + (size_t)t * pNP + col[c]);
+#pragma unroll
+      for (int c = 0; c < 6; ++c)
+        y[u][c] = *reinterpret_cast<const f4 *>(p1 + (size_t)t * pNP + col[c]);
     } else {
 #pragma unroll
       for (int c = 0; c < 6; ++c) x[u][c] = ld_h4(qkv + (size_t)t * 3 * Hl + col[c]);
     }
   }
-  if (part) {  // remaining slabs in slice order, then fp16 (partials_value)
+  after_loads();
+  if (part) {  // slabs in slice order, then fp16 (partials_value)
+    if (pS > 1)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int c = 0; c < 6; ++c) x[u][c] += y[u][c];
     const size_t slab = (size_t)T * pNP;
-    for (int sl = 1; sl < pS; ++sl)
+    for (int sl = 2; sl < pS; ++sl)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
@@ -144,13 +163,7 @@ __device__ __forceinline__ void kv_update_item(
 #pragma unroll
       for (int c = 0; c < 6; ++c) x[u][c] = round_h4(x[u][c]);
   }
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int pos = min(max(ti[u].pos, 0), max_rope_pos - 1);
-    const f4 *r = reinterpret_cast<const f4 *>(rope + ((size_t)pos * HD + i0[u]) * 2);
-    cs[u][0] = r[0];  // c0 s0 c1 s1
-    cs[u][1] = r[1];  // c2 s2 c3 s3
-  }
+
   // ---- stores
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -172,13 +185,13 @@ __device__ __forceinline__ void kv_update_item(
     uint16_t *qo = sQ ? &sQ[tl[u]][i0[u]] : qbuf + (size_t)t * Hl + h * D + i0[u];
     st_h4(qo, qlo[0], qlo[1], qlo[2], qlo[3]);
     st_h4(qo + HD, qhi[0], qhi[1], qhi[2], qhi[3]);
-    const bool store = ti[u].store_slot >= 0 && ti[u].store_slot < slots;
+    const bool store = tslot[u] >= 0 && tslot[u] < slots;
     if (store) {
-      uint16_t *kr = kc + (((size_t)ti[u].req * heads + h) * slots + ti[u].store_slot) * D + i0[u];
+      uint16_t *kr = kc + (((size_t)treq[u] * heads + h) * slots + tslot[u]) * D + i0[u];
       st_h4(kr, klo[0], klo[1], klo[2], klo[3]);
       st_h4(kr + HD, khi[0], khi[1], khi[2], khi[3]);
     }
-    if (i0[u] == 0) sSlot[tl[u]] = store ? ti[u].store_slot : -1;
+    if (i0[u] == 0) sSlot[tl[u]] = store ? tslot[u] : -1;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       sV[i0[u] + j][tl[u]] = vlo[j];
@@ -244,8 +257,8 @@ __global__ __launch_bounds__(FFMI_ATTN_QTILE * D / 8) void kv_update_kernel(
     return;
   }
   const ffmi_attn_work w = bv.work[item].w;
-  kv_update_item<D, NQ, NT>(bv, w, h, heads, slots, T, qkv, part, pS, pNP, rope, max_rope_pos,
-                            qbuf, kc, stage_wr, sV, sSlot);
+  kv_update_item<D, NQ, NT>(bv, &bv.work[item], h, heads, slots, T, qkv, part, pS, pNP, rope, max_rope_pos,
+                            qbuf, kc, stage_wr, sV, sSlot, nullptr, [] {});
   __syncthreads();
   kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
 }
@@ -313,16 +326,24 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   __shared__ float sm_l[NW][NQ];
   __shared__ __attribute__((aligned(16))) float sm_o[NW][QT][DT][4][64];
 
-  long long st[6] = {0, 0, 0, 0, 0, 0};
-  if (ST) st[0] = __builtin_amdgcn_s_memrealtime();
+  // ST: lane 0 of each wave stores its timeline straight to kv.stamps
+  long long *stp = nullptr;
+  if (ST && kv.stamps && (threadIdx.x & 63) == 0)
+    stp = kv.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + (threadIdx.x >> 6)) * 12;
+  auto stamp = [&](int i) {
+    if (ST && stp) stp[i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
   const int qi = lane & 15;
   const int g = lane >> 4;
   const int h = blockIdx.y;
   const BatchView bv = batch_view(blob);
-  const WorkDev wd = bv.work[blockIdx.x];
-  const ffmi_attn_work w = wd.w;
+  // (fields, not a copy of the WorkDev: a private copy of its rope_pos array
+  // would be indexed per lane and live in scratch)
+  const ffmi_attn_work w = bv.work[blockIdx.x].w;
+  const int clean = bv.work[blockIdx.x].clean;
   const int Hl = heads * D;
   const uint16_t *kbase = kc + ((size_t)w.req * heads + h) * slots * D;
   const uint16_t *vbase = vc + ((size_t)w.req * heads + h) * D * slots;
@@ -346,10 +367,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   };
   // FUSED: a wave's first chunk lies below every slot this step writes for
   // the request (host-computed `clean`): its loads go out before the
-  // KV-update prologue and land while the prologue runs
+  // KV-update prologue and land while the prologue runs.  (Issuing them
+  // after the prologue's own loads, unconditionally, measured slower in the
+  // model: duplicate chunks for idle waves and unclean chunks cost more port
+  // bytes than the in-order wait saves.)
   const int nchunks = (w.kv_len + 31) >> 5;
   h8 kf0[2][KS], va0[DT];
-  const bool early = FUSED && wave < nchunks && (wave + 1) * 32 <= wd.clean;
+  const bool early = FUSED && wave < nchunks && (wave + 1) * 32 <= clean;
   if (early) load_chunk(wave, kf0, va0);
 
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
@@ -373,19 +397,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
 #pragma unroll
       for (int j = 0; j < 8; ++j) vt[(size_t)j * slots] = (uint16_t)(vw[j >> 1] >> (16 * (j & 1)));
     }
+    stamp(6);
     // (2) RoPE + KV store + staging of this item's tokens, this head
-    kv_update_item<D, NQ, 64 * NW>(bv, w, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP,
-                               kv.rope, kv.max_rope_pos, qbuf, kc, kv.stage_wr, sV, sSlot,
-                               sQ);
+    kv_update_item<D, NQ, 64 * NW>(
+        bv, &bv.work[blockIdx.x], h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
+        qbuf, kc, kv.stage_wr, sV, sSlot, sQ, [] {});
+    stamp(7);
     __syncthreads();
+    stamp(8);
     kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
+    stamp(9);
     // this workgroup's stores become visible to its own loads below (the
     // (req, head) K/V lines are touched by no other workgroup this step)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
 
-  if (ST) st[1] = __builtin_amdgcn_s_memrealtime();
+  stamp(1);
   bool qvalid[QT];
   int pre[QT], tb[QT], tlen[QT];
   uint64_t tv[QT];
@@ -464,7 +492,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   };
   // wave w takes chunks w, w+NW, ... (two waves per SIMD hide each other's
   // load latency; per-wave double buffering would not fit the registers)
-  if (ST) st[2] = __builtin_amdgcn_s_memrealtime();
+  stamp(2);
   for (int c = wave; c < nchunks; c += NW) {
     if (early && c == wave) {
       compute_chunk(c * 32, kf0, va0);
@@ -475,7 +503,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     compute_chunk(c * 32, kf, va);
   }
 
-  if (ST) st[3] = __builtin_amdgcn_s_memrealtime();
+  stamp(3);
   // per-query partial sum over the 4 lane groups (same m_run in all four)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -492,7 +520,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       for (int r = 0; r < 4; ++r) sm_o[wave][qt][t][r][lane] = o[qt][t][r];
   }
   __syncthreads();
-  if (ST) st[4] = __builtin_amdgcn_s_memrealtime();
+  stamp(4);
 
   // merge: wave w finalizes d-tiles t = w, w+NW, ... of every query tile
 #pragma unroll
@@ -529,17 +557,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       *reinterpret_cast<uint2 *>(dst) = pk;
     }
   }
-  if (ST && kv.stamps) {
+  if (ST && stp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    st[5] = __builtin_amdgcn_s_memrealtime();
+    stamp(5);
     unsigned hwid;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    if (lane == 0) {
-      long long *d = kv.stamps + ((size_t)(blockIdx.y * gridDim.x + blockIdx.x) * NW + wave) * 8;
-      for (int i = 0; i < 6; ++i) d[i] = st[i];
-      d[6] = hwid;
-      d[7] = nchunks;
-    }
+    stp[10] = hwid;
+    stp[11] = nchunks;
   }
 }
 
@@ -574,14 +598,15 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
 
 // FFMI_ATTN_STAMP=1: verify-size launches record a per-wave timeline
 // {start, after prologue, before k-loop, after k-loop, after merge barrier,
-// end, HW_ID, chunks} (100 MHz realtime) for ffmi_debug_attn_stamps.
+// end, [fused] after commits, after KV update, after its barrier, after the
+// V^T stores, HW_ID, chunks} (100 MHz realtime) for ffmi_debug_attn_stamps.
 static long long *g_attn_stamps = nullptr;
 static long g_attn_stamp_waves = 0;
 static long long *attn_stamp_buf(int wgs) {
   static const bool on = getenv("FFMI_ATTN_STAMP") != nullptr;
   if (!on) return nullptr;
   if (!g_attn_stamps && hipMalloc(&g_attn_stamps, (size_t)8 << 20) != hipSuccess) return nullptr;
-  g_attn_stamp_waves = std::min<long>((long)wgs * 8, ((long)8 << 20) / 64);
+  g_attn_stamp_waves = std::min<long>((long)wgs * 8, ((long)8 << 20) / 96);
   return g_attn_stamps;
 }
 
@@ -589,7 +614,7 @@ long attn_debug_stamps(long long *dst, long max_waves) {
   if (!g_attn_stamps || max_waves <= 0) return 0;
   const long n = std::min(max_waves, g_attn_stamp_waves);
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(dst, g_attn_stamps, (size_t)n * 64, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(dst, g_attn_stamps, (size_t)n * 96, hipMemcpyDeviceToHost) != hipSuccess) return -1;
   return n;
 }
 

@@ -331,8 +331,10 @@ ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
  * returns the number of waves (<= max_waves). */
 long ffmi_debug_gemm_stamps(long long *dst, long max_waves);
 /* Diagnostics: per-wave timeline of the last verify-size attention launch when
- * FFMI_ATTN_STAMP=1 (8 int64 per wave: start, after prologue, before the key
- * loop, after it, after the merge barrier, end [100 MHz], HW_ID, chunks). */
+ * FFMI_ATTN_STAMP=1 (12 int64 per wave: start, after prologue, before the key
+ * loop, after it, after the merge barrier, end, then [one-launch path] after
+ * the commits, after the KV update, after its barrier, after the V^T stores
+ * [100 MHz]; HW_ID, chunks). */
 long ffmi_debug_attn_stamps(long long *dst, long max_waves);
 
 const char *ffmi_status_str(ffmi_status s);

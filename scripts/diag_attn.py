@@ -20,6 +20,9 @@ from hip_util import Buf, f16  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", type=int, default=128)
+    # one mode per process: fused then split in one process segfaults on the
+    # host in the split call (stamp builds only; not understood yet)
+    ap.add_argument("--modes", default="fused")
     args = ap.parse_args()
     L = F.lib()
     R, n, H, D, ctx = 8, 21, 32, 128, args.ctx
@@ -41,12 +44,12 @@ def main():
     mk = (ctypes.c_uint64 * flat.size)(*flat.ravel().tolist())
     desc = F.BatchDesc(T, R, 0, R, toks, work, (F.CommitInfo * 1)(), mk)
     F.check(L.ffmi_batch_upload(b, ctypes.byref(desc), None))
-    for mode in ("fused", "split"):
+    for mode in args.modes.split(","):
         if mode == "split":
             os.environ["FFMI_ATTN_NO_FUSE"] = "1"
         for _ in range(5):
             F.check(L.ffmi_attn_tree(h, b, qkv.ptr, out.ptr, None))
-        buf = np.zeros((R * H * 8, 8), np.int64)
+        buf = np.zeros((R * H * 8, 12), np.int64)
         m = L.ffmi_debug_attn_stamps(buf.ctypes.data, buf.shape[0])
         st = buf[:m]
         t0 = st[:, 0].min()
@@ -55,10 +58,14 @@ def main():
         names = ["start", "prologue", "setup (q, masks)", "key loop", "to merge barrier",
                  "merge + store"]
         print(f"  {names[0]:18s} p0/50/90/100 {us(st[:, 0] - t0)}")
+        if mode == "fused":
+            seq = [(0, 6, "commits"), (6, 7, "KV update"), (7, 8, "its barrier"),
+                   (8, 9, "V^T stores"), (9, 1, "drain + barrier")]
+            for a, b, nm in seq:
+                print(f"    {nm:16s} {us(st[:, b] - st[:, a])}")
         for i in range(1, 6):
             print(f"  {names[i]:18s} {us(st[:, i] - st[:, i - 1])}")
-        busy = st[st[:, 7] > (st[:, 6] * 0)]
-        print("  chunks per item", np.unique(st[:, 7]))
+        print("  chunks per item", np.unique(st[:, 11]))
 
 
 if __name__ == "__main__":
