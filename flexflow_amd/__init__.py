@@ -4,8 +4,9 @@ Import order matters on ROCm: load libffmi.so before torch so both share one
 HIP runtime (same SONAME libamdhip64.so.7).
 """
 from . import ffmi  # noqa: F401
+from .checkpoint import convert_hf_model, llama_config_from_hf  # noqa: F401
 from .serve import (Comm, GenerationResult, HashModel, Model, RequestManager,  # noqa: F401
                     generate, set_device)
 
-__all__ = ["ffmi", "Comm", "GenerationResult", "HashModel", "Model", "RequestManager",
+__all__ = ["ffmi", "convert_hf_model", "llama_config_from_hf", "Comm", "GenerationResult", "HashModel", "Model", "RequestManager",
            "generate", "set_device"]

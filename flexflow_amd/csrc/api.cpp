@@ -200,19 +200,37 @@ struct ffmi_attn {
 };
 
 // cos/sin table, same arithmetic as the reference's apply_rotary_embedding_hf
-// (inc_multihead_self_attention.cu:701-703): freq = pos * (1.0 /
-// pow(theta, 2i/d)) in the float/double mix used there, cos/sin in f32.
-static void rope_table(std::vector<float> &tab, int max_pos, int d, float theta) {
+// (inc_multihead_self_attention.cu:701-725): freq = pos * (1.0 /
+// pow(theta, 2i/d)) in the float/double mix used there, the llama3 scaling
+// branch in f32 (its wavelength is taken of pos * inv_freq, as there), and
+// cos/sin in f32.
+static void rope_table(std::vector<float> &tab, int max_pos, int d, const ffmi_attn_cfg *cfg) {
   const int h = d / 2;
   std::vector<double> inv(h);
   for (int i = 0; i < h; ++i) {
     volatile float ex = (float)2 * (float)i / (float)d;
-    inv[i] = 1.0 / (double)powf(theta, ex);
+    inv[i] = 1.0 / (double)powf(cfg->rope_theta, ex);
   }
+  const bool l3 = cfg->rope_llama3 != 0;
+  const float pi = 3.141592654f;  // CUDART_PI_F
+  const float low_wl = l3 ? (float)cfg->rope_original_max_pos / cfg->rope_low_freq_factor : 0.f;
+  const float high_wl = l3 ? (float)cfg->rope_original_max_pos / cfg->rope_high_freq_factor : 0.f;
   tab.resize((size_t)max_pos * d);
   for (int p = 0; p < max_pos; ++p)
     for (int i = 0; i < h; ++i) {
       volatile float freq = (float)((double)p * inv[i]);
+      if (l3) {
+        const float wavelen = 2 * pi / freq;
+        if (wavelen < high_wl) {
+        } else if (wavelen > low_wl) {
+          freq = freq / cfg->rope_factor;
+        } else {
+          const float smooth = ((float)cfg->rope_original_max_pos / wavelen -
+                                cfg->rope_low_freq_factor) /
+                               (cfg->rope_high_freq_factor - cfg->rope_low_freq_factor);
+          freq = (1 - smooth) * freq / cfg->rope_factor + smooth * freq;
+        }
+      }
       tab[((size_t)p * h + i) * 2 + 0] = cosf(freq);
       tab[((size_t)p * h + i) * 2 + 1] = sinf(freq);
     }
@@ -238,7 +256,7 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   if (ok && cfg->mode == FFMI_ATTN_TREE)
     ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * 2 * 2) == hipSuccess;
   std::vector<float> tab;
-  rope_table(tab, h->slots, cfg->head_dim, cfg->rope_theta);
+  rope_table(tab, h->slots, cfg->head_dim, cfg);
   if (ok) ok = hipMalloc((void **)&h->rope, tab.size() * sizeof(float)) == hipSuccess;
   if (!ok) {
     ffmi_attn_destroy(h);

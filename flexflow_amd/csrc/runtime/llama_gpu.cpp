@@ -36,6 +36,7 @@ struct Layer {
 struct LlamaGPU : public ffmi_model {
   ffmi_llama_config c{};
   ffmi_model_opts o{};
+  std::string weights_folder;  // reference-format checkpoint ("" = synthetic)
   int Hl = 0, Fl = 0, d = 0, heads_l = 0, slots = 0;
   // GEMM inputs (normed hidden, attention output, SiLU output) are kept in
   // packed activation tiles: every GEMM then reads its activation fragments
@@ -173,9 +174,63 @@ struct LlamaGPU : public ffmi_model {
     return FFMI_OK;
   }
 
+  // One tensor of a reference-format checkpoint (file_loader.cc:363-389
+  // load_from_file; names as convert_hf_model writes them): the HF name
+  // without "model.", raw fp16 or fp32 (converted, round to nearest even).
+  // k/v projections of a GQA checkpoint hold num_kv_heads * d rows; row
+  // block of query head i = kv head i / (heads / kv_heads) (:292-302).
+  ffmi_status load_tensor(uint16_t *dst, size_t n, const std::string &hf_name) {
+    std::string file = hf_name.rfind("model.", 0) == 0 ? hf_name.substr(6) : hf_name;
+    const bool kv = file.find("self_attn.k_proj") != std::string::npos ||
+                    file.find("self_attn.v_proj") != std::string::npos;
+    const int group = kv ? c.num_heads / c.num_kv_heads : 1;
+    const size_t n_file = n / group;
+    const std::string path = weights_folder + "/" + file;
+    FILE *f = fopen(path.c_str(), "rb");
+    if (!f) {
+      ffmi_set_last_error(("weight file not found: " + path).c_str(), __FILE__, __LINE__);
+      return FFMI_ERR_INVALID;
+    }
+    fseek(f, 0, SEEK_END);
+    const long bytes = ftell(f);
+    fseek(f, 0, SEEK_SET);
+    std::vector<uint16_t> h16(n_file);
+    bool ok = false;
+    if (bytes == (long)(n_file * 2)) {
+      ok = fread(h16.data(), 2, n_file, f) == n_file;
+    } else if (bytes == (long)(n_file * 4)) {
+      std::vector<float> h32(n_file);
+      ok = fread(h32.data(), 4, n_file, f) == n_file;
+      for (size_t i = 0; ok && i < n_file; ++i) {
+        const _Float16 v = (_Float16)h32[i];
+        memcpy(&h16[i], &v, 2);
+      }
+    }
+    fclose(f);
+    if (!ok) {
+      ffmi_set_last_error(("weight file has the wrong size: " + path).c_str(), __FILE__, __LINE__);
+      return FFMI_ERR_INVALID;
+    }
+    if (group > 1) {  // [kv_heads * d][H] -> [heads * d][H]
+      const size_t row_block = n_file / c.num_kv_heads;  // d rows of one head
+      std::vector<uint16_t> rep(n);
+      for (int i = 0; i < c.num_heads; ++i)
+        memcpy(rep.data() + (size_t)i * row_block, h16.data() + (size_t)(i / group) * row_block,
+               row_block * 2);
+      h16.swap(rep);
+    }
+    FFMI_HIP(hipMemcpy(dst, h16.data(), n * 2, hipMemcpyHostToDevice));
+    return FFMI_OK;
+  }
+
   ffmi_status init() {
     const int H = c.hidden, F = c.intermediate, V = c.vocab_size, P = o.tp_size;
-    FFMI_CHECK(c.num_kv_heads == c.num_heads, FFMI_ERR_UNSUPPORTED);  // MHA
+    // GQA checkpoints load with K/V replicated per query head (the
+    // reference's layout); synthetic weights are MHA only
+    FFMI_CHECK(c.num_kv_heads == c.num_heads ||
+                   (!weights_folder.empty() && c.num_kv_heads > 0 &&
+                    c.num_heads % c.num_kv_heads == 0),
+               FFMI_ERR_UNSUPPORTED);
     FFMI_CHECK(H % c.num_heads == 0 && c.num_heads % P == 0 && F % P == 0, FFMI_ERR_INVALID);
     d = H / c.num_heads;
     FFMI_CHECK(d == 64 || d == 128, FFMI_ERR_UNSUPPORTED);
@@ -217,6 +272,7 @@ struct LlamaGPU : public ffmi_model {
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
     TRY(alloc(&tmp, tmp_elems));
     auto fill = [&](uint16_t *dst, size_t n, const std::string &name, int kind) {
+      if (!weights_folder.empty()) return load_tensor(dst, n, name);
       return ffmi_fill_weight(dst, n, name.c_str(), o.weight_seed, kind, (ffmi_stream)stream);
     };
     TRY(alloc(&embed, (size_t)V * H));
@@ -271,6 +327,11 @@ struct LlamaGPU : public ffmi_model {
       ac.max_tokens = Tm;
       ac.qk_scale = 1.0f / sqrtf((float)d);
       ac.rope_theta = c.rope_theta;
+      ac.rope_llama3 = c.rope_llama3;
+      ac.rope_factor = c.rope_factor;
+      ac.rope_low_freq_factor = c.rope_low_freq_factor;
+      ac.rope_high_freq_factor = c.rope_high_freq_factor;
+      ac.rope_original_max_pos = c.rope_original_max_pos;
       ac.out_layout = packed ? 1 : 0;
       TRY(ffmi_attn_create(&ac, &L.attn));
       int sl = 0;
@@ -491,6 +552,8 @@ ffmi_status create_llama_gpu(const ffmi_llama_config *cfg, const ffmi_model_opts
   m->mode = o->mode;
   m->c = *cfg;
   m->o = *o;
+  if (o->weights_folder && o->weights_folder[0]) m->weights_folder = o->weights_folder;
+  m->o.weights_folder = nullptr;
   ffmi_status st = m->init();
   if (st != FFMI_OK) {
     delete m;

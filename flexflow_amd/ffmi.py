@@ -52,25 +52,33 @@ class AttnCfg(ctypes.Structure):
     _fields_ = [("mode", c_int), ("num_heads", c_int), ("head_dim", c_int),
                 ("max_requests", c_int), ("max_seq_len", c_int), ("max_tree_tokens", c_int),
                 ("max_tokens", c_int), ("qk_scale", c_float), ("rope_theta", c_float),
-                ("out_layout", c_int)]
+                ("out_layout", c_int), ("rope_llama3", c_int), ("rope_factor", c_float),
+                ("rope_low_freq_factor", c_float), ("rope_high_freq_factor", c_float),
+                ("rope_original_max_pos", c_int)]
 
 
 class LlamaConfig(ctypes.Structure):
     _fields_ = [("num_layers", c_int), ("vocab_size", c_int), ("num_heads", c_int),
                 ("num_kv_heads", c_int), ("hidden", c_int), ("intermediate", c_int),
-                ("rms_eps", c_float), ("rope_theta", c_float)]
+                ("rms_eps", c_float), ("rope_theta", c_float), ("rope_llama3", c_int),
+                ("rope_factor", c_float), ("rope_low_freq_factor", c_float),
+                ("rope_high_freq_factor", c_float), ("rope_original_max_pos", c_int)]
 
     @classmethod
     def from_dict(cls, d):
         return cls(d["num_layers"], d["vocab_size"], d["num_heads"],
                    d.get("num_kv_heads", d["num_heads"]), d["hidden"], d["intermediate"],
-                   d.get("rms_eps", 1e-6), d.get("rope_theta", 10000.0))
+                   d.get("rms_eps", 1e-6), d.get("rope_theta", 10000.0),
+                   d.get("rope_llama3", 0), d.get("rope_factor", 1.0),
+                   d.get("rope_low_freq_factor", 1.0), d.get("rope_high_freq_factor", 4.0),
+                   d.get("rope_original_max_pos", 8192))
 
 
 class ModelOpts(ctypes.Structure):
     _fields_ = [("mode", c_int), ("tp_rank", c_int), ("tp_size", c_int), ("comm", c_void_p),
                 ("max_requests", c_int), ("max_tokens", c_int), ("max_seq_len", c_int),
-                ("max_tree_tokens", c_int), ("weight_seed", c_uint64), ("use_graphs", c_int)]
+                ("max_tree_tokens", c_int), ("weight_seed", c_uint64), ("use_graphs", c_int),
+                ("weights_folder", ctypes.c_char_p)]
 
 
 class RMConfig(ctypes.Structure):

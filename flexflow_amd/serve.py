@@ -18,13 +18,16 @@ class Model:
 
     def __init__(self, config: dict, mode: str = "inc", *, max_requests=8, max_tokens=128,
                  max_seq_len=512, max_tree_tokens=23, weight_seed=20250117, tp_rank=0,
-                 tp_size=1, comm=None):
+                 tp_size=1, comm=None, weights_folder: Optional[str] = None):
+        """weights_folder: a checkpoint in the reference's per-tensor format
+        (see checkpoint.convert_hf_model); None: seeded synthetic weights."""
         L = F.lib()
         self.config = dict(config)
         self.mode = mode
         cfg = F.LlamaConfig.from_dict(config)
         opts = F.ModelOpts(self.MODES[mode], tp_rank, tp_size, comm.handle if comm else None,
-                           max_requests, max_tokens, max_seq_len, max_tree_tokens, weight_seed, 0)
+                           max_requests, max_tokens, max_seq_len, max_tree_tokens, weight_seed, 0,
+                           weights_folder.encode() if weights_folder else None)
         h = ctypes.c_void_p()
         F.check(L.ffmi_model_create(ctypes.byref(cfg), ctypes.byref(opts), ctypes.byref(h)),
                 "ffmi_model_create")

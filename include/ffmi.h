@@ -121,6 +121,11 @@ typedef struct {
   int out_layout;      /* 0: out [T][heads*head_dim] row-major;
                           1: packed activation tiles (feeds ffmi_linear with
                           FFMI_X_PACKED; heads*head_dim % 32 == 0)          */
+  /* llama3 RoPE frequency scaling (inc_multihead_self_attention.cu:703-722;
+   * rope_llama3 = 0: plain HF RoPE, the other fields ignored)               */
+  int rope_llama3;
+  float rope_factor, rope_low_freq_factor, rope_high_freq_factor;
+  int rope_original_max_pos;
 } ffmi_attn_cfg;
 
 typedef struct ffmi_attn ffmi_attn;
@@ -234,6 +239,10 @@ ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *name,
 typedef struct {
   int num_layers, vocab_size, num_heads, num_kv_heads, hidden, intermediate;
   float rms_eps, rope_theta;
+  /* llama3 RoPE scaling (llama.h:53-65), as in ffmi_attn_cfg */
+  int rope_llama3;
+  float rope_factor, rope_low_freq_factor, rope_high_freq_factor;
+  int rope_original_max_pos;
 } ffmi_llama_config;
 
 typedef enum {
@@ -252,6 +261,13 @@ typedef struct {
   int max_tree_tokens;       /* max_spec_tree_token_num                        */
   uint64_t weight_seed;      /* synthetic weights (orc_gen_weight spec)        */
   int use_graphs;            /* capture per-shape hipGraphs (0/1)              */
+  /* Checkpoint in the reference's format (file_loader.cc:217-361,
+   * serve/models/llama.py convert_hf_model): one raw fp16 or fp32 file per
+   * tensor, named as the HF parameter without "model." ("embed_tokens.weight",
+   * "layers.0.self_attn.q_proj.weight", ..., "norm.weight", "lm_head.weight").
+   * K/V projections of GQA checkpoints are replicated to every query head as
+   * the reference does (file_loader.cc:292-302).  NULL: synthetic weights. */
+  const char *weights_folder;
 } ffmi_model_opts;
 
 typedef struct ffmi_model ffmi_model;

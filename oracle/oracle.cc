@@ -166,20 +166,40 @@ extern "C" void orc_silu_mul(const float *A, const float *B, float *out,
 }
 
 // RoPE table: freq = pos * (1.0 / pow(theta, 2i/d)) with the reference's
-// float/double mix (inc_multihead_self_attention.cu:701-703), cos/sin in f32.
-extern "C" void orc_rope_table(float *tab, int max_pos, int d, float theta) {
+// float/double mix (inc_multihead_self_attention.cu:701-703), the llama3
+// scaling branch in f32 (:704-722: its wavelength is 2*pi / freq of the
+// already position-scaled freq), cos/sin in f32.
+extern "C" void orc_rope_table_llama3(float *tab, int max_pos, int d, float theta, int llama3,
+                                      float factor, float low_ff, float high_ff, int orig_max) {
   const int h = d / 2;
   std::vector<double> inv(h);
   for (int i = 0; i < h; ++i) {
     float ex = (float)2 * (float)i / (float)d;
     inv[i] = 1.0 / (double)powf(theta, ex);
   }
+  const float pi = 3.141592654f;
+  const float low_wl = llama3 ? (float)orig_max / low_ff : 0.f;
+  const float high_wl = llama3 ? (float)orig_max / high_ff : 0.f;
   for (int p = 0; p < max_pos; ++p)
     for (int i = 0; i < h; ++i) {
       float freq = (float)((double)p * inv[i]);
+      if (llama3) {
+        float wavelen = 2 * pi / freq;
+        if (wavelen < high_wl) {
+        } else if (wavelen > low_wl) {
+          freq = freq / factor;
+        } else {
+          float smooth = ((float)orig_max / wavelen - low_ff) / (high_ff - low_ff);
+          freq = (1 - smooth) * freq / factor + smooth * freq;
+        }
+      }
       tab[((size_t)p * h + i) * 2 + 0] = cosf(freq);
       tab[((size_t)p * h + i) * 2 + 1] = sinf(freq);
     }
+}
+
+extern "C" void orc_rope_table(float *tab, int max_pos, int d, float theta) {
+  orc_rope_table_llama3(tab, max_pos, d, theta, 0, 1.f, 1.f, 1.f, 1);
 }
 
 // apply_rotary_embedding_hf (inc_multihead_self_attention.cu:664-738):

@@ -70,6 +70,8 @@ void orc_silu_mul(const float *A, const float *B, float *out, size_t n,
 void orc_rope_head(float *x, int d, int pos, float theta, int fp16);
 /* cos/sin table used by both the oracle and the GPU: tab[(pos*(d/2)+i)*2+{0,1}] */
 void orc_rope_table(float *tab, int max_pos, int d, float theta);
+void orc_rope_table_llama3(float *tab, int max_pos, int d, float theta, int llama3, float factor,
+                           float low_ff, float high_ff, int orig_max);
 /* One query row against `n_keys` key/value rows (head_dim d) with a
  * visibility vector (1 = visible).  Softmax with __expf and 1/(sum+1e-6) as
  * in compute_attention_kernel_generation_kernel (inc_..._attention.cu:372-623)

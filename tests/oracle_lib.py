@@ -47,6 +47,9 @@ def lib():
                                                          ctypes.c_float, ctypes.c_int]
         L.orc_silu_mul.argtypes = [_f32p, _f32p, _f32p, ctypes.c_size_t, ctypes.c_int]
         L.orc_rope_table.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float]
+        L.orc_rope_table_llama3.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                            ctypes.c_int, ctypes.c_float, ctypes.c_float,
+                                            ctypes.c_float, ctypes.c_int]
         L.orc_rope_head.argtypes = [_f32p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
                                     ctypes.c_int]
         L.orc_attention_row.argtypes = [_f32p, _f32p, _f32p, _u8p, ctypes.c_int,
@@ -128,9 +131,13 @@ def silu_mul(A, B, fp16=1):
     return out
 
 
-def rope_table(max_pos, d, theta):
-    tab = np.empty(max_pos * d, np.float32)
-    lib().orc_rope_table(fp(tab), max_pos, d, theta)
+def rope_table(max_pos, d, theta, llama3=None):
+    """llama3: None or (factor, low_freq_factor, high_freq_factor, original_max_pos)."""
+    tab = np.zeros((max_pos, d), np.float32)
+    if llama3:
+        lib().orc_rope_table_llama3(fp(tab), max_pos, d, theta, 1, *llama3)
+    else:
+        lib().orc_rope_table(fp(tab), max_pos, d, theta)
     return tab
 
 

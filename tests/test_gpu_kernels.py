@@ -250,12 +250,13 @@ class AttnCase:
     """Builds token-info batches for ffmi_attn_* and the matching oracle."""
 
     def __init__(self, mode, heads=2, d=128, max_requests=4, max_seq=96, tree=32, max_tokens=128,
-                 out_layout=0):
+                 out_layout=0, theta=10000.0, llama3=None):
         self.heads, self.d = heads, d
         self.Hl = heads * d
         self.out_layout = out_layout
+        l3 = (1,) + tuple(llama3) if llama3 else (0, 1.0, 1.0, 4.0, 8192)
         cfg = F.AttnCfg(mode, heads, d, max_requests, max_seq, tree, max_tokens,
-                        1.0 / np.sqrt(d), 10000.0, out_layout)
+                        1.0 / np.sqrt(d), theta, out_layout, *l3)
         self.h = ctypes.c_void_p()
         F.check(L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(self.h)))
         self.b = ctypes.c_void_p()
@@ -263,7 +264,7 @@ class AttnCase:
         slots = ctypes.c_int()
         L.ffmi_attn_kv_ptrs(self.h, None, None, ctypes.byref(slots))
         self.slots = slots.value
-        self.tab = O.rope_table(self.slots, d, 10000.0).reshape(self.slots, d // 2, 2)
+        self.tab = O.rope_table(self.slots, d, theta, llama3).reshape(self.slots, d // 2, 2)
         self.kc = {}  # (req, slot) -> (k_rot [heads,d], v [heads,d])
         self.mode = mode
 
@@ -349,6 +350,20 @@ def test_attention_inc_prefill_then_decode(d, layout):
         close16(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)), exact_frac=0.98)
     infos = [(7, 20, 0, 20, 21, 0, 0, 0), (7, 37, 1, 37, 38, 0, 0, 0)] + \
             [(7, p, 2, p, p + 1, 0, 0, 0) for p in range(10, 15)]
+    out, qs = c.run(infos, rng=rng)
+    for t, i in enumerate(infos):
+        close16(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)), exact_frac=0.98)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+def test_attention_llama3_rope_scaling(d):
+    """llama3 frequency scaling (inc_multihead_self_attention.cu:703-722) in
+    the handle's RoPE table: original_max_position 64 puts the three
+    wavelength branches inside the first 60 positions."""
+    rng = np.random.default_rng(200 + d)
+    c = AttnCase(F.ATTN_INC, d=d, theta=500000.0, llama3=(8.0, 1.0, 4.0, 64))
+    lens = {0: 33, 1: 57}
+    infos = [(5, p, r, p, p + 1, 0, 0, 0) for r, n in lens.items() for p in range(n)]
     out, qs = c.run(infos, rng=rng)
     for t, i in enumerate(infos):
         close16(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)), exact_frac=0.98)
