@@ -188,6 +188,11 @@ def main():
     ap.add_argument("--no-incr", action="store_true", help="skip the incr-decoding side run")
     ap.add_argument("--profile", type=int, default=1, help="op profiling level in timed steps")
     ap.add_argument("--layers", type=int, default=0, help="override LLM layer count (debug)")
+    ap.add_argument("--llm-weights", default=None,
+                    help="reference-format checkpoint folder with config.json (default: "
+                         "seeded synthetic LLaMA-7B)")
+    ap.add_argument("--ssm-weights", default=None,
+                    help="reference-format checkpoint folder of the SSM (default: synthetic 68M)")
     args = ap.parse_args()
 
     rank = int(os.environ.get("RANK", 0))
@@ -203,7 +208,8 @@ def main():
         uid = ctrl.bcast(fa.Comm.unique_id() if rank == 0 else b"")
         comm = fa.Comm(uid, world, rank)
 
-    llm_cfg = dict(LLAMA_7B)
+    llm_cfg = fa.llama_config_from_hf(args.llm_weights) if args.llm_weights else dict(LLAMA_7B)
+    ssm_cfg = fa.llama_config_from_hf(args.ssm_weights) if args.ssm_weights else dict(LLAMA_68M)
     if args.layers:
         llm_cfg["num_layers"] = args.layers
     B, P, D = args.batch, args.prefill, args.decode
@@ -221,16 +227,17 @@ def main():
     if spec:
         llm = fa.Model(llm_cfg, "tree", max_requests=B, max_tokens=verify_cap,
                        max_seq_len=rm_kw["max_sequence_length"], max_tree_tokens=tree,
-                       weight_seed=20250117, tp_rank=rank, tp_size=world, comm=comm)
-        ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=verify_cap,
+                       weight_seed=20250117, tp_rank=rank, tp_size=world, comm=comm,
+                       weights_folder=args.llm_weights)
+        ssm = fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=verify_cap,
                        max_seq_len=rm_kw["max_sequence_length"], max_tree_tokens=tree,
-                       weight_seed=68)
+                       weight_seed=68, weights_folder=args.ssm_weights)
         rm = fa.RequestManager(spec_tree_width=widths, **rm_kw)
         rm.register_ssm_model(ssm)
     else:
         llm = fa.Model(llm_cfg, "inc", max_requests=B, max_tokens=mtb,
                        max_seq_len=rm_kw["max_sequence_length"], weight_seed=20250117,
-                       tp_rank=rank, tp_size=world, comm=comm)
+                       tp_rank=rank, tp_size=world, comm=comm, weights_folder=args.llm_weights)
         rm = fa.RequestManager(**rm_kw)
     init_s = time.time() - t_init
 
@@ -270,10 +277,14 @@ def main():
         "value": round(value, 2), "unit": "tokens/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(1000 * elapsed / args.steps, 2),
         "higher_is_better": True, "scaling": "strong", "vs_baseline": None, "dtype": "f16",
-        "data": "synthetic (seeded random weights and prompts)",
+        "data": ("synthetic prompts, checkpoint weights" if args.llm_weights else
+                 "synthetic (seeded random weights and prompts)"),
         "config": {"workload": ("llama7b_specinfer_llama68m" if spec else "llama7b_incr") +
-                   f"_b{B}_p{P}_d{D}", "model": "LLaMA-7B (random init)",
-                   "ssm": "LLaMA-68M (random init)" if spec else None,
+                   f"_b{B}_p{P}_d{D}",
+                   "model": (f"LLaMA ({args.llm_weights})" if args.llm_weights
+                             else "LLaMA-7B (random init)"),
+                   "ssm": ((f"LLaMA ({args.ssm_weights})" if args.ssm_weights
+                            else "LLaMA-68M (random init)") if spec else None),
                    "global_batch": B, "prefill": P, "decode": D, "seq_len": max_len,
                    "parallelism": f"tp{world}", "tree_widths": list(widths) if spec else None,
                    "max_tokens_per_batch": mtb, "layers": llm_cfg["num_layers"]},
@@ -312,7 +323,8 @@ def main():
                  "launches": v["launches"]} for kk, v in ops.items()}
     if rank == 0 and world == 1 and spec and not args.no_incr:
         inc = fa.Model(llm_cfg, "inc", max_requests=B, max_tokens=mtb,
-                       max_seq_len=rm_kw["max_sequence_length"], weight_seed=20250117)
+                       max_seq_len=rm_kw["max_sequence_length"], weight_seed=20250117,
+                       weights_folder=args.llm_weights)
         rmi = fa.RequestManager(**rm_kw)
         run_generate(rmi, inc, prompts, max_len, False)  # warm
         t1 = time.time()
