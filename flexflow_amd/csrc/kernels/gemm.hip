@@ -465,7 +465,7 @@ static long g_stamp_entries = 0;
 
 // Sum the S fp32 partial slabs in slice order, then the epilogue; one thread
 // per 4 consecutive output columns (16-B slab loads, 8-B fp16 store).
-template <int EPI>
+template <int EPI, int MAXS>
 __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__restrict__ Y,
                                    int T, int N, int NTILES, int S, int yp) {
   const int NP = NTILES * 16;
@@ -475,19 +475,25 @@ __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__
   const int m = (int)(idx / nq), n = (int)(idx % nq) * 4;
   const size_t slab = (size_t)T * NP;
   f4 acc, up;
-  if (EPI == 0) {
-    const float *src = Ypart + (size_t)m * NP + n;
-    acc = *reinterpret_cast<const f4 *>(src);
-    for (int s = 1; s < S; ++s) acc += *reinterpret_cast<const f4 *>(src + s * slab);
-  } else {
-    const float *src = Ypart + (size_t)m * NP + (n >> 4) * 32 + (n & 15);
-    acc = *reinterpret_cast<const f4 *>(src);
-    up = *reinterpret_cast<const f4 *>(src + 16);
-    for (int s = 1; s < S; ++s) {
-      acc += *reinterpret_cast<const f4 *>(src + s * slab);
-      up += *reinterpret_cast<const f4 *>(src + s * slab + 16);
-    }
+  // all MAXS >= S slab loads go out before the first add (one memory round
+  // trip, not S); indices past S re-read the last slab and are not added
+  f4 pa[MAXS], pu[MAXS];
+  const float *src = EPI == 0 ? Ypart + (size_t)m * NP + n
+                              : Ypart + (size_t)m * NP + (n >> 4) * 32 + (n & 15);
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    const float *q = src + (size_t)min(s, S - 1) * slab;
+    pa[s] = *reinterpret_cast<const f4 *>(q);
+    if (EPI) pu[s] = *reinterpret_cast<const f4 *>(q + 16);
   }
+  acc = pa[0];
+  if (EPI) up = pu[0];
+#pragma unroll
+  for (int s = 1; s < MAXS; ++s)
+    if (s < S) {
+      acc += pa[s];
+      if (EPI) up += pu[s];
+    }
   uint16_t o[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
@@ -548,7 +554,7 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       const int n = sscanf(q, "%d:%d:%d,%d", &a, &b, &c, &d);
       if (n == 4 && a == N && b == K) ntw = c, S = d;
       else if (n != 4 && sscanf(q, "%d,%d", &a, &b) == 2) ntw = a, S = b;
-      if ((ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) && S >= 1 && S <= KT) {
+      if ((ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) && S >= 1 && S <= std::min(KT, 8)) {
         p.NTW = ntw, p.S = S;
         break;
       }
@@ -611,12 +617,19 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   if (S > 1) {
     const long total = (long)T * ((N + 3) / 4);
     const unsigned blocks = (unsigned)((total + 255) / 256);
-    if (epi)
-      hipLaunchKernelGGL(gemm_reduce_kernel<1>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S, yp);
-    else
-      hipLaunchKernelGGL(gemm_reduce_kernel<0>, dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                         ntiles, S, yp);
+#define FFMI_RED(E, MS)                                                                    \
+  hipLaunchKernelGGL((gemm_reduce_kernel<E, MS>), dim3(blocks), dim3(256), 0, s, ws, Y, T, N, \
+                     ntiles, S, yp)
+    if (epi) {
+      if (S <= 2) FFMI_RED(1, 2);
+      else if (S <= 4) FFMI_RED(1, 4);
+      else FFMI_RED(1, 8);
+    } else {
+      if (S <= 2) FFMI_RED(0, 2);
+      else if (S <= 4) FFMI_RED(0, 4);
+      else FFMI_RED(0, 8);
+    }
+#undef FFMI_RED
   }
   return hipGetLastError();
 }

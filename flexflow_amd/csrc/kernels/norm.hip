@@ -43,17 +43,20 @@ __device__ __forceinline__ T block_sum(T v, T *scratch) {
 // One workgroup of NT threads per row, MAXC 8-element chunks per thread; every
 // load of the row (x1, x2 or its split-K slabs, and w) is issued before the
 // reduction, so a row costs one memory round trip.
-template <int NT, int MAXC>
+template <int NT, int MAXC, int MAXS>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
     uint16_t *__restrict__ out, int H, float eps, int out_packed,
-    const float *__restrict__ x2p, int pS, int pNP) {
+    const float *__restrict__ x2p, int pS, int pNP, const char *__restrict__ gather) {
   __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int T = gridDim.x;
   const int nchunk = H >> 3;
-  const uint16_t *a = x1 + (size_t)row * H;
+  // gather: x1 is the embedding table and row t reads its token's row (the
+  // embedding lookup fused into the first layer's norm; res_out gets the copy)
+  const uint16_t *a = gather ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
+                             : x1 + (size_t)row * H;
   const uint16_t *b = x2 ? x2 + (size_t)row * H : nullptr;
   uint4 v[MAXC], wv[MAXC];
   float ss = 0.f;
@@ -66,12 +69,21 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       if (b || x2p) {
         uint4 xb;
         if (x2p) {  // x2 = deferred split-K slabs of the producing GEMM, summed in order
+          // all MAXS >= pS slab loads are issued before the first add (a
+          // runtime-bounded loop would pay one memory round trip per slab);
+          // indices past pS re-read the last slab and are not added
           const float *q = x2p + (size_t)row * pNP + ch * 8;
-          f4 lo = *reinterpret_cast<const f4 *>(q), hi = *reinterpret_cast<const f4 *>(q + 4);
-          for (int sl = 1; sl < pS; ++sl) {
-            lo += *reinterpret_cast<const f4 *>(q + (size_t)sl * T * pNP);
-            hi += *reinterpret_cast<const f4 *>(q + (size_t)sl * T * pNP + 4);
+          f4 slo[MAXS], shi[MAXS];
+#pragma unroll
+          for (int sl = 0; sl < MAXS; ++sl) {
+            const float *qs = q + (size_t)min(sl, pS - 1) * T * pNP;
+            slo[sl] = *reinterpret_cast<const f4 *>(qs);
+            shi[sl] = *reinterpret_cast<const f4 *>(qs + 4);
           }
+          f4 lo = slo[0], hi = shi[0];
+#pragma unroll
+          for (int sl = 1; sl < MAXS; ++sl)
+            if (sl < pS) lo += slo[sl], hi += shi[sl];
           uint16_t hb[8];
 #pragma unroll
           for (int q4 = 0; q4 < 4; ++q4) {
@@ -88,6 +100,8 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) r[q] = __hadd2(pa[q], pb[q]);  // correctly rounded
         xa = *reinterpret_cast<uint4 *>(r);
+        *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
+      } else if (gather) {
         *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
       }
       v[c] = xa;
@@ -122,16 +136,26 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s, bool out_packed, Partials x2p) {
+                          hipStream_t s, bool out_packed, Partials x2p, const char *gather) {
+  if (gather && (x2 || x2p.S > 0 || !res_out)) return hipErrorInvalidValue;
   if (T <= 0) return hipSuccess;
   if (out_packed && H % 32) return hipErrorInvalidValue;
   const int op = out_packed ? 1 : 0;
   const int nchunk = H / 8;
   if (nchunk > 4096) return hipErrorInvalidValue;
   const float *pp = x2p.S > 0 ? x2p.p : nullptr;
-#define FFMI_RMS(NT, MC)                                                                    \
-  hipLaunchKernelGGL((rmsnorm_kernel<NT, MC>), dim3(T), dim3(NT), 0, s, x1, x2, w, res_out, \
-                     out, H, eps, op, pp, x2p.S, x2p.NP)
+  if (pp && x2p.S > 8) return hipErrorInvalidValue;
+  const int ms = !pp || x2p.S <= 1 ? 1 : x2p.S <= 2 ? 2 : x2p.S <= 4 ? 4 : 8;
+#define FFMI_RMS2(NT, MC, MS)                                                                   \
+  hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS>), dim3(T), dim3(NT), 0, s, x1, x2, w, res_out, \
+                     out, H, eps, op, pp, x2p.S, x2p.NP, gather)
+#define FFMI_RMS(NT, MC)                                   \
+  do {                                                     \
+    if (ms == 1) FFMI_RMS2(NT, MC, 1);                     \
+    else if (ms == 2) FFMI_RMS2(NT, MC, 2);                \
+    else if (ms == 4) FFMI_RMS2(NT, MC, 4);                \
+    else FFMI_RMS2(NT, MC, 8);                             \
+  } while (0)
   if (nchunk <= 128) FFMI_RMS(128, 1);
   else if (nchunk <= 256) FFMI_RMS(256, 1);
   else if (nchunk <= 512) FFMI_RMS(512, 1);
@@ -139,6 +163,7 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   else if (nchunk <= 2048) FFMI_RMS(1024, 2);
   else FFMI_RMS(1024, 4);
 #undef FFMI_RMS
+#undef FFMI_RMS2
   return hipGetLastError();
 }
 

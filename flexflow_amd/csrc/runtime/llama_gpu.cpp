@@ -434,9 +434,7 @@ struct LlamaGPU : public ffmi_model {
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
     TRY(ffmi::batch_copy(batch, blob_bytes, stream, record_upload));
     const bool ptail = prof_on(0, T);
-    int pr = prof_begin(ptail);
-    TRY(ffmi_embedding(batch, embed, res, H, s));
-    prof_end(pr, EMBED, (double)T * H * 4, 0);
+    int pr = 0;
     ffmi::Partials down_part;
     for (int l = 0; l < c.num_layers; ++l) {
       Layer &L = layers[l];
@@ -446,9 +444,13 @@ struct LlamaGPU : public ffmi_model {
       // (rope-store for qkv; the residual norm for o/down when there is no
       // all-reduce in between) instead of a separate reduce pass
       const int XP = packed ? FFMI_X_PACKED : 0;
-      FFMI_HIP(ffmi::launch_rmsnorm(res, l == 0 ? nullptr : proj, L.in_norm, res, h, T, H, eps,
-                                    stream, packed, l == 0 ? ffmi::Partials() : down_part));
-      prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 2 : 4), 0);
+      // layer 0: the embedding lookup gathers straight into the first norm
+      // (embedding_kernels.cu:233-244; res = the looked-up rows)
+      FFMI_HIP(ffmi::launch_rmsnorm(l == 0 ? embed : res, l == 0 ? nullptr : proj, L.in_norm, res,
+                                    h, T, H, eps, stream, packed,
+                                    l == 0 ? ffmi::Partials() : down_part,
+                                    l == 0 ? batch->dev : nullptr));
+      prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
       pr = prof_begin(on);
       ffmi::Partials qkv_part;
       FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
