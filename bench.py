@@ -30,6 +30,8 @@ import flexflow_amd as fa  # noqa: E402  (load libffmi before anything else)
 
 LLAMA_7B = dict(num_layers=32, vocab_size=32000, num_heads=32, num_kv_heads=32, hidden=4096,
                 intermediate=11008, rms_eps=1e-6, rope_theta=10000.0)
+LLAMA_65B = dict(num_layers=80, vocab_size=32000, num_heads=64, num_kv_heads=64, hidden=8192,
+                 intermediate=22016, rms_eps=1e-5, rope_theta=10000.0)
 LLAMA_68M = dict(num_layers=2, vocab_size=32000, num_heads=12, num_kv_heads=12, hidden=768,
                  intermediate=3072, rms_eps=1e-6, rope_theta=10000.0)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
@@ -171,6 +173,25 @@ def pmc_traffic(kernel):
         if d.get("kernel") == kernel:
             d["source"] = os.path.relpath(f, ROOT)
             return d
+    return None
+
+
+MID_GATE_UP = "ffmi::gemm_mid_kernel<3, 6, 4, 1, false, true>"
+
+
+def pmc_mfma(hip_kernel):
+    """MFMA utilisation (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x kernel
+    cycles)) of one kernel from the separate rocprofv3 --pmc pass
+    (scripts/mfma_summary.py -> profiles/rNN_pmc_mfma.json); None if absent."""
+    import glob
+    for f in reversed(sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_mfma.json")))):
+        try:
+            d = json.load(open(f))
+        except (OSError, ValueError):
+            continue
+        for k in d.get("kernels", []):
+            if k["kernel"] == hip_kernel.replace("void ", ""):
+                return {"mfma_util": k["mfma_util"], "source": os.path.relpath(f, ROOT)}
     return None
 
 
@@ -317,6 +338,10 @@ def main():
         if tr:
             out["roofline"]["traffic"] = tr["fetch_bytes_per_launch"]
             out["roofline"]["traffic_source"] = tr["source"]
+            mf = pmc_mfma(tr.get("hip_kernel", MID_GATE_UP))
+            if mf:
+                out["roofline"]["mfma_util"] = mf["mfma_util"]
+                out["roofline"]["mfma_util_source"] = mf["source"]
         out["op_breakdown_sampled"] = {
             kk: {"avg_us": round(1000 * v["ms"] / v["launches"], 2),
                  "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] else None,

@@ -1,11 +1,11 @@
 """Per-rank compute of the TP=N SpecInfer step, on ONE GPU.
 
-Builds the LLaMA-7B verify model as shard 0 of N (heads / FFN columns /
+Builds the LLaMA-7B (or --model 65b: LLaMA-65B, configs D/E) verify model as shard 0 of N (heads / FFN columns /
 rows of o and down) over a 1-rank communicator, so its all-reduces are
 no-ops: the numbers are the per-rank GEMM / attention / norm time of the
 bench at --gpus N, WITHOUT the all-reduce cost (tokens are meaningless).
 
-    python scripts/tp_shard_bench.py --tp 8
+    python scripts/tp_shard_bench.py --tp 8 [--model 65b] [--mode incr]
 """
 import argparse
 import json
@@ -17,26 +17,35 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import flexflow_amd as fa  # noqa: E402
-from bench import LLAMA_68M, LLAMA_7B, make_prompts  # noqa: E402
+from bench import LLAMA_65B, LLAMA_68M, LLAMA_7B, make_prompts  # noqa: E402
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--tp", type=int, default=8)
     ap.add_argument("--steps", type=int, default=1)
+    ap.add_argument("--model", choices=["7b", "65b"], default="7b")
+    ap.add_argument("--mode", choices=["spec", "incr"], default="spec")
     args = ap.parse_args()
+    cfg = LLAMA_65B if args.model == "65b" else LLAMA_7B
+    spec = args.mode == "spec"
     fa.set_device(0)
     comm = fa.Comm(fa.Comm.unique_id(), 1, 0)
     B, P, D, tree, mtb = 8, 128, 128, 23, 1024
     rm_kw = dict(max_requests_per_batch=B, max_tokens_per_batch=mtb,
                  max_spec_tree_token_num=tree, max_sequence_length=512)
-    llm = fa.Model(LLAMA_7B, "tree", max_requests=B, max_tokens=mtb + tree * B, max_seq_len=512,
-                   max_tree_tokens=tree, tp_rank=0, tp_size=args.tp, comm=comm)
-    ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=mtb + tree * B, max_seq_len=512,
-                   max_tree_tokens=tree, weight_seed=68)
-    rm = fa.RequestManager(spec_tree_width=(1, 1, 3), **rm_kw)
-    rm.register_ssm_model(ssm)
-    prompts = make_prompts(B, P - 1, LLAMA_7B["vocab_size"])
+    if spec:
+        llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=mtb + tree * B, max_seq_len=512,
+                       max_tree_tokens=tree, tp_rank=0, tp_size=args.tp, comm=comm)
+        ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=mtb + tree * B,
+                       max_seq_len=512, max_tree_tokens=tree, weight_seed=68)
+        rm = fa.RequestManager(spec_tree_width=(1, 1, 3), **rm_kw)
+        rm.register_ssm_model(ssm)
+    else:
+        llm = fa.Model(cfg, "inc", max_requests=B, max_tokens=mtb, max_seq_len=512,
+                       tp_rank=0, tp_size=args.tp, comm=comm)
+        rm = fa.RequestManager(**rm_kw)
+    prompts = make_prompts(B, P - 1, cfg["vocab_size"])
     fa.generate(rm, llm, prompts, max_length=P + D)  # warm
     llm.set_profiling(1)
     t0 = time.time()
@@ -46,7 +55,7 @@ def main():
     st = rm.stats()
     ops = llm.op_stats()
     print(json.dumps({
-        "tp": args.tp, "s_per_generate": round(dt, 3),
+        "model": args.model, "mode": args.mode, "tp": args.tp, "s_per_generate": round(dt, 3),
         "tokens_per_s_without_allreduce": round(sum(len(r.output_tokens) - len(r.input_tokens)
                                                     for r in res) / dt, 1),
         "llm_ms": round(st.llm_us / 1000 / (args.steps + 1), 1),
