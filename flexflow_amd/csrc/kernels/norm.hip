@@ -5,6 +5,8 @@
 // reduction and the scale pass (one read + one write per element).  Unlike
 // the reference (which launches every buffer row, rms_norm_kernels.cu:133-134)
 // only the T active rows are processed.
+#include <algorithm>
+
 #include "../ffmi_internal.h"
 
 namespace ffmi {
@@ -228,9 +230,11 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
   __syncthreads();
   mx = fmaxf(fmaxf(fscratch[0], fscratch[1]), fmaxf(fscratch[2], fscratch[3]));
   __syncthreads();
-  float se = 0.f;
-  for (int i = threadIdx.x; i < V; i += 256) se += expf(h2f_(x[i]) - mx);
-  const float sum = block_sum256(se, fscratch);
+  // float exponentials summed in double: S = the oracle's float(double sum)
+  __shared__ double dscratch[4];
+  double se = 0.0;
+  for (int i = threadIdx.x; i < V; i += 256) se += (double)expf(h2f_(x[i]) - mx);
+  const float sum = (float)block_sum256(se, dscratch);
   int chosen[4] = {-1, -1, -1, -1};
   for (int r = 0; r < k; ++r) {
     // key = (p bits << 32) | (~idx): max key = largest p, lowest index
@@ -263,22 +267,34 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
   }
 }
 
-// Register-resident variant: one 512-thread workgroup per row reads the row
-// ONCE as 16-B vectors (NV per thread) and does max, sum and the k selection
-// rounds from registers.  Same arithmetic and tie rule as the kernel above.
-template <int NV>
-__global__ __launch_bounds__(512) void softmax_topk_reg_kernel(
+// Register-resident variant: one TPB-thread workgroup per row reads the row
+// ONCE as 16-B vectors (NV per thread) and keeps it in registers.
+//  * S = float(sum of float exp(x_i - M) accumulated in double): the oracle's
+//    float(double sum), whatever the summation order.
+//  * p_i is computed only for CANDIDATES: p is non-decreasing in x, and the
+//    k-th largest of the per-wave maxima, L, is <= the row's k-th largest
+//    logit, so every member of the top-k (ties included) has fp16 p >= p(L),
+//    i.e. an unrounded p_i above the lower rounding boundary of p(L): x_i >=
+//    M + log(boundary * S).  That threshold (lowered by a margin that covers
+//    the float error of exp/div/log) excludes all but a handful of logits, and
+//    the 32000 exp + correctly rounded divisions of a full p pass go away.
+//  * k rounds of a block-wide (p desc, idx asc) selection over the candidates.
+template <int TPB, int NV>
+__global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
     float *__restrict__ probs) {
-  __shared__ float fscratch[8];
-  __shared__ unsigned long long kscratch[8];
+  constexpr int NW = TPB / 64;
+  // ONE shared array: wave maxima / sums / selection keys
+  __shared__ double sh[NW + 2];
+  float *fsh = reinterpret_cast<float *>(sh);
+  unsigned long long *ksh = reinterpret_cast<unsigned long long *>(sh);
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nvec = V >> 3;
   const uint4 *x = reinterpret_cast<const uint4 *>(logits + (size_t)row * V);
   uint4 r[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const int i = v * 512 + tid;
+    const int i = v * TPB + tid;
     r[v] = i < nvec ? x[i] : make_uint4(0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u);
   }
   auto elem = [&](int v, int e) -> float {
@@ -292,73 +308,99 @@ __global__ __launch_bounds__(512) void softmax_topk_reg_kernel(
     for (int e = 0; e < 8; ++e) mx = fmaxf(mx, elem(v, e));
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if (lane == 0) fscratch[wv] = mx;
+  if (lane == 0) fsh[wv] = mx;
   __syncthreads();
-  mx = fscratch[0];
+  float wmax[NW];
 #pragma unroll
-  for (int q = 1; q < 8; ++q) mx = fmaxf(mx, fscratch[q]);
+  for (int q = 0; q < NW; ++q) wmax[q] = fsh[q];
   __syncthreads();
-  float se = 0.f;
+  float M = wmax[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) M = fmaxf(M, wmax[q]);
+  // L = k-th largest wave maximum (k <= 4 <= NW): a lower bound of the k-th
+  // largest logit
+  float L = -INFINITY;
+  {
+    float top[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      float v = wmax[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float hi = fmaxf(top[j], v), lo = fminf(top[j], v);
+        top[j] = hi, v = lo;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j == k - 1) L = top[j];
+  }
+  double se = 0.0;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
-    if (v * 512 + tid < nvec)
+    if (v * TPB + tid < nvec)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) se += expf(elem(v, e) - mx);
+      for (int e = 0; e < 8; ++e) se += (double)expf(elem(v, e) - M);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
-  if (lane == 0) fscratch[wv] = se;
+  if (lane == 0) sh[wv] = se;
   __syncthreads();
-  float sum = 0.f;
+  double sd = 0.0;
 #pragma unroll
-  for (int q = 0; q < 8; ++q) sum += fscratch[q];
-  // p_i = fp16(exp(x_i - max) / sum), computed once and kept in place of the
-  // logits; a selected element is marked 0xFFFF (a NaN pattern p never takes)
-  uint16_t *ph = reinterpret_cast<uint16_t *>(r);
-#pragma unroll
-  for (int v = 0; v < NV; ++v)
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      ph[v * 8 + e] = (v * 512 + tid) * 8 + e < V
-                          ? f2h_(__fdiv_rn(expf(h2f_(ph[v * 8 + e]) - mx), sum))
-                          : (uint16_t)0xFFFF;
+  for (int q = 0; q < NW; ++q) sd += sh[q];
+  const float S = (float)sd;
+  // candidate threshold from p(L): its lower fp16 rounding boundary, minus a
+  // margin of 2^-10 in x (>> the float error of exp, the division and log)
+  // (finite: logits set to -inf -- taken ones -- are never candidates)
+  float thr = -3.402823466e38f;
+  {
+    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    if (pL > 1) {
+      const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
+      thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
+    }
+  }
+  __syncthreads();
+  // keys: (p + 1) << 32 | ~idx, 0 = not a candidate / taken
   for (int rd = 0; rd < k; ++rd) {
-    // key = (p + 1) << 32 | ~idx: max key = largest p, then lowest index
     unsigned long long best = 0;
 #pragma unroll
     for (int v = 0; v < NV; ++v)
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
-        const uint16_t p = ph[v * 8 + e];
-        const unsigned i = (unsigned)((v * 512 + tid) * 8 + e);
-        const unsigned long long key =
-            p == 0xFFFF ? 0ull
-                        : ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
-        best = key > best ? key : best;
+        const float xv = elem(v, e);
+        const unsigned i = (unsigned)((v * TPB + tid) * 8 + e);
+        if (xv >= thr && (int)i < V) {
+          const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+          const unsigned long long key =
+              ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
+          best = key > best ? key : best;
+        }
       }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) {
       unsigned long long other = __shfl_xor(best, o);
       best = other > best ? other : best;
     }
+    if (lane == 0) ksh[wv] = best;
     __syncthreads();
-    if (lane == 0) kscratch[wv] = best;
-    __syncthreads();
-    unsigned long long b = kscratch[0];
+    unsigned long long b = ksh[0];
 #pragma unroll
-    for (int q = 1; q < 8; ++q) b = kscratch[q] > b ? kscratch[q] : b;
+    for (int q = 1; q < NW; ++q) b = ksh[q] > b ? ksh[q] : b;
+    __syncthreads();
     const unsigned idx = 0xffffffffu - (unsigned)(b & 0xffffffffu);
-    const uint16_t pbest = (uint16_t)((b >> 32) - 1u);
     if (tid == 0) {
       ids[(size_t)row * k + rd] = (int)idx;
-      if (probs) probs[(size_t)row * k + rd] = h2f_(pbest);
+      if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
     }
-    if (rd + 1 < k && (idx >> 3) % 512 == (unsigned)tid) {  // owner marks it taken
+    if (rd + 1 < k && (idx >> 3) % TPB == (unsigned)tid) {  // owner marks it taken (-inf)
 #pragma unroll
       for (int v = 0; v < NV; ++v)
-        if ((unsigned)(v * 512 + tid) == (idx >> 3)) {
+        if ((unsigned)(v * TPB + tid) == (idx >> 3)) {
+          uint16_t *ph = reinterpret_cast<uint16_t *>(&r[v]);
 #pragma unroll
           for (int e = 0; e < 8; ++e)
-            if ((unsigned)e == (idx & 7)) ph[v * 8 + e] = 0xFFFF;
+            if ((unsigned)e == (idx & 7)) ph[e] = 0xfc00;
         }
     }
   }
@@ -368,16 +410,16 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
                          float *probs, hipStream_t s) {
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4) return hipErrorInvalidValue;
-  const int nv = (V / 8 + 511) / 512;
-  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 8) {
-    if (nv <= 1)
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<1>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
-    else if (nv <= 2)
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<2>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
-    else if (nv <= 4)
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<4>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
-    else
-      hipLaunchKernelGGL(softmax_topk_reg_kernel<8>, dim3(T), dim3(512), 0, s, logits, V, k, ids, probs);
+  const int nv = (V / 8 + 1023) / 1024;
+  // (NV = 8 at 1024 threads would spill: larger vocabularies take the loop kernel)
+  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 4) {
+#define FFMI_SMR(NV)                                                                        \
+  hipLaunchKernelGGL((softmax_topk_reg_kernel<1024, NV>), dim3(T), dim3(1024), 0, s, logits, V, \
+                     k, ids, probs)
+    if (nv <= 1) FFMI_SMR(1);
+    else if (nv <= 2) FFMI_SMR(2);
+    else FFMI_SMR(4);
+#undef FFMI_SMR
   } else {
     hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
   }

@@ -231,6 +231,34 @@ def test_softmax_argmax_topk_exact(V):
         np.testing.assert_array_equal(pr.get(), rp)
 
 
+@pytest.mark.parametrize("T,V", [(24, 32000), (200, 32000), (3, 4096), (5, 65536)])
+def test_softmax_topk_chunked_ties(T, V):
+    """Chunked path (one workgroup per 2048 logits, last chunk merges): exact
+    ties spread over several chunks resolve to the lowest indices, and rows of
+    equal logits pick 0, 1, 2."""
+    rng = np.random.default_rng(T + V)
+    logits = f16(rng.standard_normal((T, V)) * 3)
+    logits[0, :] = f16(0.5)                       # all equal
+    for j in (V - 1, 7000 % V, 2049 % V, 4095):    # one maximum in several chunks
+        logits[1, j] = f16(12.0)
+    logits[2, V // 2] = f16(10.0)                  # near-ties that fp16 p collapses
+    logits[2, V // 2 + 1] = f16(10.0 - 2 ** -7)
+    logits[2, 3] = f16(10.0 - 2 ** -7)
+    lb = Buf(logits)
+    for k in (1, 3, 4):
+        ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+        F.check(L.ffmi_arg_topk(lb.ptr, T, V, k, ids.ptr, pr.ptr, None))
+        rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+        assert np.array_equal(ids.get(), rid), np.argwhere(ids.get() != rid)[:5]
+        np.testing.assert_array_equal(pr.get(), rp)
+        assert ids.get()[0].tolist() == list(range(k))
+    # repeated launches re-arm the per-row arrival counters
+    for _ in range(3):
+        ids = Buf.empty((T,), np.int32)
+        F.check(L.ffmi_argmax(lb.ptr, T, V, ids.ptr, None, None))
+        assert ids.get().tolist() == O.softmax_argmax(logits.astype(np.float32), fp16=1)[0].tolist()
+
+
 # ---------------------------------------------------------------- attention
 def pack_act_np(X):
     """numpy twin of ffmi_pack_activations: [T][K] -> [T/16][K/32][64 lanes][8]."""
