@@ -124,17 +124,35 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[u][i], b[u][j], acc[i][j],
                                                             0, 0, 0);
   }
-  for (; kt < ke; ++kt) {
-    h8 b[NT];
+  // tail (< U k-steps; with a small K -- the SSM, K = 768 over 4-8 waves --
+  // the whole loop): every load of the batch is issued before the first MFMA
+  // (one memory round trip, not one per k-step).  Steps past ke re-load the
+  // last step (valid addresses, no branch) and add a zero weight fragment.
+  if (kt < ke) {
+    const int rem = ke - kt;
+    h8 b[U - 1][NT];
+    h8 a[U - 1][MT];
 #pragma unroll
-    for (int j = 0; j < NT; ++j)
-      b[j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)kt * 512);
-#pragma unroll
-    for (int i = 0; i < MT; ++i) {
-      h8 a = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kt * XS);
+    for (int u = 0; u < U - 1; ++u) {
+      const int kk = min(kt + u, ke - 1);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b[j], acc[i][j], 0, 0, 0);
+        b[u][j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)kk * 512);
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+        a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
+    }
+    const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u) {
+      if (u >= rem)
+#pragma unroll
+        for (int j = 0; j < NT; ++j) b[u][j] = zero;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(a[u][i], b[u][j], acc[i][j], 0, 0, 0);
     }
   }
 
@@ -243,12 +261,35 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
   int ntiles = (N + 15) / 16;
   if (epi == FFMI_EPI_SILU_MUL)
     return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp);
-  if (MT >= 4 && ntiles >= 512)
+  // diagnostics: FFMI_SKINNY="NT,KW" forces the tile count and K-split waves
+  // of every unsplit skinny launch (A/B runs, scripts/gemm_bench.py)
+  static int fnt = -1, fkw = 0;
+  if (fnt < 0) {
+    fnt = 0;
+    if (const char *e = getenv("FFMI_SKINNY")) (void)sscanf(e, "%d,%d", &fnt, &fkw);
+  }
+  if (fnt > 0 && S == 1 && MT <= 2) {
+    if (fnt == 1 && fkw == 4) return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 1 && fkw == 8) return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 2 && fkw == 4) return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 2 && fkw == 8) return run<MT, 2, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+  }
+  // wide layers (lm_head): two tiles per workgroup once there are >= 2 row
+  // tiles (SSM lm_head at T = 24: 16.1 -> 12.3 us warm; at one row tile a
+  // single tile stays faster: LLaMA-7B lm_head T = 8 cold 47.8 vs 55.8 us)
+  if (MT >= 2 && ntiles >= 512)
     return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
   // 8-wave groups only where the accumulators fit 2 waves/SIMD (no spills)
   if (ntiles >= 512 || MT >= 8)
     return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
-  return run<MT, 1, (MT >= 8 ? 4 : 8), U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+  // ... and where each wave still gets a full batch of U k-steps (K = 768 of
+  // the SSM: 4 waves x 6 k-steps beat 8 x 3, qkv T = 24: 5.7 -> 4.2 us)
+  if ((KT + S - 1) / S >= 8 * U)
+    return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+  return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
 }
 
 // ---------------------------------------------------------------------------

@@ -269,7 +269,7 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
 
 // Register-resident variant: one TPB-thread workgroup per row reads the row
 // ONCE as 16-B vectors (NV per thread) and keeps it in registers.
-//  * S = float(sum of float exp(x_i - M) accumulated in double): the oracle's
+//  * S = float(sum of exp(x_i - M) accumulated in double): the oracle's
 //    float(double sum), whatever the summation order.
 //  * p_i is computed only for CANDIDATES: p is non-decreasing in x, and the
 //    k-th largest of the per-wave maxima, L, is <= the row's k-th largest
@@ -335,12 +335,15 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     for (int j = 0; j < 4; ++j)
       if (j == k - 1) L = top[j];
   }
+  // the sum uses the hardware exp2 (__expf, a few ulp): over 32000 terms
+  // accumulated in double its error stays orders of magnitude below the
+  // float rounding of S; the p values that are compared use the accurate expf
   double se = 0.0;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (v * TPB + tid < nvec)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) se += (double)expf(elem(v, e) - M);
+      for (int e = 0; e < 8; ++e) se += (double)__expf(elem(v, e) - M);
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
   if (lane == 0) sh[wv] = se;
