@@ -58,7 +58,7 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
 // workgroup reduces its K slice over its waves and writes an fp32 partial
 // slab [S][T][NTILES*16] that the consumer combines in slice order
 // (Partials, the M-split kernel's slab layout).
-template <int MT, int NT, int KW, int U, int EPI>
+template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
@@ -102,6 +102,63 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
   }
 
   int kt = kb;
+  if constexpr (PIPE) {
+    // software pipeline over batches of UP = U/2 k-steps, two register sets:
+    // the next batch's loads are issued before this batch's MFMAs, so each
+    // wave keeps UP..2*UP k-steps in flight
+    constexpr int UP = U / 2;
+    const int nb = (ke - kt) / UP;
+    if (nb > 0) {
+      h8 bA[UP][NT], aA[UP][MT], bB[UP][NT], aB[UP][MT];
+      auto ld = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT], int k0) {
+#pragma unroll
+        for (int u = 0; u < UP; ++u)
+#pragma unroll
+          for (int j = 0; j < NT; ++j)
+            bb[u][j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)(k0 + u) * 512);
+#pragma unroll
+        for (int u = 0; u < UP; ++u)
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+            aa[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)(k0 + u) * XS);
+      };
+      auto mm = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT]) {
+#pragma unroll
+        for (int u = 0; u < UP; ++u)
+#pragma unroll
+          for (int i = 0; i < MT; ++i)
+#pragma unroll
+            for (int j = 0; j < NT; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aa[u][i], bb[u][j], acc[i][j],
+                                                                0, 0, 0);
+      };
+      ld(bA, aA, kt);
+      int q = 0;
+      for (; q + 2 < nb; q += 2) {
+        ld(bB, aB, kt + UP);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bA, aA);
+        __builtin_amdgcn_sched_barrier(0);
+        ld(bA, aA, kt + 2 * UP);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bB, aB);
+        __builtin_amdgcn_sched_barrier(0);
+        kt += 2 * UP;
+      }
+      if (q + 1 < nb) {  // two batches left
+        ld(bB, aB, kt + UP);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bA, aA);
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bB, aB);
+        kt += 2 * UP;
+      } else {  // one batch left
+        __builtin_amdgcn_sched_barrier(0);
+        mm(bA, aA);
+        kt += UP;
+      }
+    }
+  }
   for (; kt + U <= ke; kt += U) {
     h8 b[U][NT];
     h8 a[U][MT];
@@ -115,6 +172,10 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)(kt + u) * XS);
+    // keep the whole batch of loads ahead of the MFMAs: left alone the
+    // scheduler interleaves them and reuses registers, leaving ~7 loads in
+    // flight per wave with a vmcnt wait before almost every MFMA
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -142,6 +203,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
     }
+    __builtin_amdgcn_sched_barrier(0);
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (int u = 0; u < U - 1; ++u) {
@@ -236,8 +298,20 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
   const int ncb = (NTILES + NT - 1) / NT;
   dim3 grid(ncb, S);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI>), grid, dim3(KW * 64), lds, s, X,
-                     Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
+  // software-pipelined k-loop once every wave has >= 2 full batches (LLaMA-7B
+  // decode at T = 8, cold: qkv 21.2 -> 19.5 us, gate/up 39.1 -> 36.8, lm_head
+  // 49.5 -> 46.1); short loops (the SSM, K = 768) keep the batched form, which
+  // the pipeline slowed (SSM lm_head warm 9.3 -> 12.1 us).
+  // FFMI_SKINNY_PIPE=0/1 forces it off/on (A/B runs).
+  static const int force = getenv("FFMI_SKINNY_PIPE") ? atoi(getenv("FFMI_SKINNY_PIPE")) : -1;
+  const int per_wave = ((KT + S - 1) / S + KW - 1) / KW;
+  const bool pipe = force >= 0 ? force != 0 : per_wave >= 2 * U;
+  if (pipe)
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, true>), grid, dim3(KW * 64), lds, s,
+                       X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
+  else
+    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI>), grid, dim3(KW * 64), lds, s, X,
+                       Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
   return hipGetLastError();
 }
 
