@@ -442,7 +442,7 @@ __device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *_
 __device__ long long *g_gemm_stamps;
 __device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false>
+template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false, bool ULD = false>
 __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
@@ -469,7 +469,11 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
 #pragma unroll
   for (int p = 0; p < PPT; ++p) {
     bj[p] = wave + 4 * p;
-    const int t = min(tile0 + bj[p], NTILES - 1);
+    // ULD: waves past the last tile re-load the block's last tile (an L2 hit
+    // beside the wave that owns it) so that EVERY wave issues PPT weight loads
+    // per k-step: loads behind a wave-dependent branch are invisible to the
+    // compiler's vmcnt counting, which then waits for ~2 ring slots, not PF-1
+    const int t = min(tile0 + (ULD ? min(bj[p], NTW - 1) : bj[p]), NTILES - 1);
     bsrc[p] = Wp + (size_t)t * KT * 512 + lane * 8;
   }
   // X row-major [T][K] (16 rows x 64 B per fragment load), or XP: packed
@@ -508,7 +512,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
     }
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
@@ -534,7 +538,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
       // B(kt+1) lives in ring slot (Q+1) % PF
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
@@ -707,9 +711,19 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   if (S > 1 && (!ws || ws_bytes < need)) S = 1;  // no workspace: un-split (slower)
   dim3 grid(nblk, S, mblocks);
   static const bool stamp = getenv("FFMI_GEMM_STAMP") != nullptr;
-#define FFMI_MID(E, ST, XPK)                                                                  \
-  hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK>), grid, dim3(256), 0, s, X, Wp, \
-                     Y, ws, T, N, K, KT, ntiles, S, yp)
+  // unconditional weight loads (ULD) whenever NTW % 4 != 0 (gate/up T = 168:
+  // 55.9 -> 51.2 us, qkv 37.2 -> 34.6 us in scripts/gemm_bench.py);
+  // FFMI_MID_ULD=0 turns them off (A/B runs)
+  static const bool uld = !getenv("FFMI_MID_ULD") || atoi(getenv("FFMI_MID_ULD")) != 0;
+#define FFMI_MID(E, ST, XPK)                                                                      \
+  do {                                                                                            \
+    if (uld && NTW % 4)                                                                           \
+      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK, true>), grid, dim3(256), 0, s, \
+                         X, Wp, Y, ws, T, N, K, KT, ntiles, S, yp);                               \
+    else                                                                                          \
+      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK>), grid, dim3(256), 0, s, X,   \
+                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);                                  \
+  } while (0)
   if (stamp && !epi && stamp_buf()) {
     g_stamp_entries = (long)nblk * S * mblocks * 4;
     if (xpacked) FFMI_MID(0, true, true);
