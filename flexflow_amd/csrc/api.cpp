@@ -4,7 +4,10 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -505,10 +508,96 @@ extern "C" ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *nam
 // RCCL all-reduce (RCCL over xGMI; the reference: ncclAllReduce,
 // allreduce_kernels.cu:67-74)
 // ---------------------------------------------------------------------------
+// In-process shard group (ffmi_comm_create_local): the ranks are host
+// threads of ONE process stepping their shards on one device.  All-reduce =
+// barrier, rank 0 sums every rank's buffer into a group scratch, barrier, each
+// rank copies the sum, barrier.  Barriers time out (a shard that failed
+// mid-step returns an error to the others instead of hanging them).
+struct LocalGroup {
+  int n = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0;
+  long gen = 0;
+  bool broken = false;
+  std::vector<const void *> bufs;
+  void *tmp = nullptr;
+  size_t tmp_bytes = 0;
+  ~LocalGroup() {
+    if (tmp) (void)hipFree(tmp);
+  }
+  bool barrier() {
+    std::unique_lock<std::mutex> lk(mu);
+    if (broken) return false;
+    const long g = gen;
+    if (++arrived == n) {
+      arrived = 0;
+      ++gen;
+      cv.notify_all();
+      return true;
+    }
+    if (!cv.wait_for(lk, std::chrono::seconds(120), [&] { return gen != g || broken; }) || broken) {
+      broken = true;
+      cv.notify_all();
+      return false;
+    }
+    return true;
+  }
+};
+
 struct ffmi_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
+  std::shared_ptr<LocalGroup> local;
 };
+
+extern "C" ffmi_status ffmi_comm_create_local(int nranks, ffmi_comm **out) {
+  FFMI_CHECK(out && nranks >= 1 && nranks <= 8, FFMI_ERR_INVALID);
+  auto g = std::make_shared<LocalGroup>();
+  g->n = nranks;
+  g->bufs.assign(nranks, nullptr);
+  for (int r = 0; r < nranks; ++r) {
+    out[r] = new ffmi_comm();
+    out[r]->nranks = nranks;
+    out[r]->rank = r;
+    out[r]->local = g;
+  }
+  return FFMI_OK;
+}
+
+static ffmi_status local_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
+                                   int dtype, hipStream_t s) {
+  LocalGroup &g = *c->local;
+  const size_t bytes = count * (dtype == FFMI_F16 ? 2 : 4);
+  g.bufs[c->rank] = in;
+  FFMI_HIP(hipStreamSynchronize(s));  // this rank's partial is complete
+  FFMI_CHECK(g.barrier(), FFMI_ERR_NCCL);
+  ffmi_status st = FFMI_OK;
+  if (c->rank == 0) {
+    if (g.tmp_bytes < bytes) {
+      if (g.tmp) (void)hipFree(g.tmp);
+      g.tmp = nullptr;
+      g.tmp_bytes = 0;
+      if (hipMalloc(&g.tmp, bytes) == hipSuccess) g.tmp_bytes = bytes;
+    }
+    if (!g.tmp) {
+      st = FFMI_ERR_OOM;
+    } else if (ffmi::launch_group_sum(g.bufs.data(), g.n, g.tmp, count, dtype, s) != hipSuccess ||
+               hipStreamSynchronize(s) != hipSuccess) {
+      st = FFMI_ERR_HIP;
+    }
+  }
+  if (!g.barrier() || st != FFMI_OK) {
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.broken = true;
+    g.cv.notify_all();
+    return st != FFMI_OK ? st : FFMI_ERR_NCCL;
+  }
+  FFMI_HIP(hipMemcpyAsync(out, g.tmp, bytes, hipMemcpyDeviceToDevice, s));
+  FFMI_HIP(hipStreamSynchronize(s));
+  FFMI_CHECK(g.barrier(), FFMI_ERR_NCCL);  // nobody reuses tmp before all copied
+  return FFMI_OK;
+}
 
 extern "C" ffmi_status ffmi_comm_unique_id(void *id_out) {
   FFMI_CHECK(id_out, FFMI_ERR_INVALID);
@@ -545,6 +634,8 @@ extern "C" void ffmi_comm_destroy(ffmi_comm *c) {
 extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
                                       int dtype, ffmi_stream stream) {
   FFMI_CHECK(c && in && out, FFMI_ERR_INVALID);
+  if (c->local && c->nranks > 1)
+    return local_allreduce(c, in, out, count, dtype, (hipStream_t)stream);
   if (c->nranks == 1) {
     if (in != out) {
       const size_t esz = dtype == FFMI_F16 ? 2 : 4;

@@ -126,6 +126,8 @@ hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
                            size_t n, hipStream_t s);
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
                          float *probs, hipStream_t s);
+hipError_t launch_group_sum(const void *const *bufs, int n, void *out, size_t count, int dtype,
+                            hipStream_t s);
 
 hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_t *qkv,
                             Partials qkvp, uint16_t *qbuf, uint16_t *kc, uint16_t *vc,

@@ -429,4 +429,44 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   return hipGetLastError();
 }
 
+// Sum of the ranks' buffers of an in-process shard group (ffmi_comm_create_
+// local): out = sum over r in rank order, fp16 accumulated in fp32 then
+// rounded once (RCCL's ring sums in fp16 in ring order; both are within an
+// fp16 ulp of the exact sum).
+struct GroupBufs {
+  const void *p[8];
+};
+__global__ void group_sum_kernel(GroupBufs b, int n, void *__restrict__ out, size_t count,
+                                 int dtype) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < count;
+       i += (size_t)gridDim.x * blockDim.x) {
+    if (dtype == FFMI_F16) {
+      float a = 0.f;
+      for (int r = 0; r < n; ++r) a += h2f_(reinterpret_cast<const uint16_t *>(b.p[r])[i]);
+      reinterpret_cast<uint16_t *>(out)[i] = f2h_(a);
+    } else if (dtype == FFMI_F32) {
+      float a = 0.f;
+      for (int r = 0; r < n; ++r) a += reinterpret_cast<const float *>(b.p[r])[i];
+      reinterpret_cast<float *>(out)[i] = a;
+    } else {
+      int a = 0;
+      for (int r = 0; r < n; ++r) a += reinterpret_cast<const int *>(b.p[r])[i];
+      reinterpret_cast<int *>(out)[i] = a;
+    }
+  }
+}
+
+hipError_t launch_group_sum(const void *const *bufs, int n, void *out, size_t count, int dtype,
+                            hipStream_t s) {
+  if (n < 1 || n > 8) return hipErrorInvalidValue;
+  if (count == 0) return hipSuccess;
+  GroupBufs b;
+  for (int r = 0; r < 8; ++r) b.p[r] = bufs[r < n ? r : 0];
+  size_t blocks = (count + 255) / 256;
+  if (blocks > 4096) blocks = 4096;
+  hipLaunchKernelGGL(group_sum_kernel, dim3((unsigned)blocks), dim3(256), 0, s, b, n, out, count,
+                     dtype);
+  return hipGetLastError();
+}
+
 }  // namespace ffmi

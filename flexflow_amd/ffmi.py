@@ -130,6 +130,7 @@ SIGNATURES = {
     "ffmi_residual_rmsnorm": (c_int, [c_void_p] * 5 + [c_int, c_int, c_float, c_void_p]),
     "ffmi_comm_unique_id": (c_int, [c_void_p]),
     "ffmi_comm_create": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "ffmi_comm_create_local": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "ffmi_comm_destroy": (None, [c_void_p]),
     "ffmi_allreduce": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "ffmi_embedding": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),

@@ -85,6 +85,19 @@ class Comm:
         F.check(F.lib().ffmi_comm_create(buf, nranks, rank, ctypes.byref(h)), "comm create")
         self.handle = h
 
+    @classmethod
+    def local_group(cls, nranks: int):
+        """In-process shard group: one communicator per host thread stepping
+        a TP shard on this process's device (ffmi_comm_create_local)."""
+        arr = (ctypes.c_void_p * nranks)()
+        F.check(F.lib().ffmi_comm_create_local(nranks, arr), "local group")
+        out = []
+        for r in range(nranks):
+            c = cls.__new__(cls)
+            c.handle = ctypes.c_void_p(arr[r])
+            out.append(c)
+        return out
+
     def close(self):
         if getattr(self, "handle", None):
             F.lib().ffmi_comm_destroy(self.handle)

@@ -209,6 +209,11 @@ typedef struct ffmi_comm ffmi_comm;
 #define FFMI_UNIQUE_ID_BYTES 128
 ffmi_status ffmi_comm_unique_id(void *id_out /* FFMI_UNIQUE_ID_BYTES */);
 ffmi_status ffmi_comm_create(const void *id, int nranks, int rank, ffmi_comm **out);
+/* In-process shard group: `nranks` (<= 8) communicators for host THREADS of
+ * one process that step the TP shards of a model on one device (the
+ * reference's TP-invariance tests, cpp_inference_tests.sh:203-217, on a
+ * single GPU).  out[r] is rank r; destroy each with ffmi_comm_destroy. */
+ffmi_status ffmi_comm_create_local(int nranks, ffmi_comm **out);
 void ffmi_comm_destroy(ffmi_comm *c);
 ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
                            int dtype, ffmi_stream stream);
