@@ -45,7 +45,12 @@ __device__ __forceinline__ T block_sum(T v, T *scratch) {
 // One workgroup of NT threads per row, MAXC 8-element chunks per thread; every
 // load of the row (x1, x2 or its split-K slabs, and w) is issued before the
 // reduction, so a row costs one memory round trip.
-template <int NT, int MAXC, int MAXS>
+// SRC (compile time, so that the loads are straight-line code: behind
+// runtime branches the compiler reused a loaded register as the slab address
+// and waited for the x1 load before issuing the slabs -- two round trips):
+//   0: x1 only   1: x1 + x2 (fp16)   2: x1 + split-K slabs   3: gather (x1 =
+//   embedding table, rows picked by the step's token ids)
+template <int NT, int MAXC, int MAXS, int SRC>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
@@ -57,53 +62,61 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   const int nchunk = H >> 3;
   // gather: x1 is the embedding table and row t reads its token's row (the
   // embedding lookup fused into the first layer's norm; res_out gets the copy)
-  const uint16_t *a = gather ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
-                             : x1 + (size_t)row * H;
-  const uint16_t *b = x2 ? x2 + (size_t)row * H : nullptr;
+  const uint16_t *a = SRC == 3 ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
+                               : x1 + (size_t)row * H;
   uint4 v[MAXC], wv[MAXC];
+  // every load of the row first (slabs, x2, x1, w), then the arithmetic;
+  // x2 = the deferred split-K slabs of the producing GEMM summed in order,
+  // folded per chunk when a thread holds several chunks (register budget)
+  uint4 xb[MAXC];
+  f4 slo[MAXS], shi[MAXS];
+  auto fold = [&]() {
+    f4 lo = slo[0], hi = shi[0];
+#pragma unroll
+    for (int sl = 1; sl < MAXS; ++sl)
+      if (sl < pS) lo += slo[sl], hi += shi[sl];
+    uint16_t hb[8];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      hb[q4] = f2h_(lo[q4]);
+      hb[q4 + 4] = f2h_(hi[q4]);
+    }
+    return *reinterpret_cast<uint4 *>(hb);
+  };
+#pragma unroll
+  for (int c = 0; c < MAXC; ++c) {
+    const int ch = min((int)threadIdx.x + c * NT, nchunk - 1);  // clamped: no branch
+    if (SRC == 2) {
+      const float *q = x2p + (size_t)row * pNP + ch * 8;
+#pragma unroll
+      for (int sl = 0; sl < MAXS; ++sl) {
+        const float *qs = q + (size_t)min(sl, pS - 1) * T * pNP;
+        slo[sl] = *reinterpret_cast<const f4 *>(qs);
+        shi[sl] = *reinterpret_cast<const f4 *>(qs + 4);
+      }
+    }
+    if (SRC == 1) xb[c] = *reinterpret_cast<const uint4 *>(x2 + (size_t)row * H + ch * 8);
+    v[c] = *reinterpret_cast<const uint4 *>(a + ch * 8);
+    wv[c] = *reinterpret_cast<const uint4 *>(w + ch * 8);
+    if (SRC == 2 && MAXC > 1) xb[c] = fold();
+  }
+  if (SRC == 2 && MAXC == 1) xb[0] = fold();
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * NT;
     if (ch < nchunk) {
-      wv[c] = *reinterpret_cast<const uint4 *>(w + ch * 8);
-      uint4 xa = *reinterpret_cast<const uint4 *>(a + ch * 8);
-      if (b || x2p) {
-        uint4 xb;
-        if (x2p) {  // x2 = deferred split-K slabs of the producing GEMM, summed in order
-          // all MAXS >= pS slab loads are issued before the first add (a
-          // runtime-bounded loop would pay one memory round trip per slab);
-          // indices past pS re-read the last slab and are not added
-          const float *q = x2p + (size_t)row * pNP + ch * 8;
-          f4 slo[MAXS], shi[MAXS];
-#pragma unroll
-          for (int sl = 0; sl < MAXS; ++sl) {
-            const float *qs = q + (size_t)min(sl, pS - 1) * T * pNP;
-            slo[sl] = *reinterpret_cast<const f4 *>(qs);
-            shi[sl] = *reinterpret_cast<const f4 *>(qs + 4);
-          }
-          f4 lo = slo[0], hi = shi[0];
-#pragma unroll
-          for (int sl = 1; sl < MAXS; ++sl)
-            if (sl < pS) lo += slo[sl], hi += shi[sl];
-          uint16_t hb[8];
-#pragma unroll
-          for (int q4 = 0; q4 < 4; ++q4) {
-            hb[q4] = f2h_(lo[q4]);
-            hb[q4 + 4] = f2h_(hi[q4]);
-          }
-          xb = *reinterpret_cast<uint4 *>(hb);
-        } else {
-          xb = *reinterpret_cast<const uint4 *>(b + ch * 8);
-        }
+      uint4 xa = v[c];
+      if (SRC == 1 || SRC == 2) {
+        const uint4 xbb = xb[c];
         const __half2 *pa = reinterpret_cast<const __half2 *>(&xa);
-        const __half2 *pb = reinterpret_cast<const __half2 *>(&xb);
+        const __half2 *pb = reinterpret_cast<const __half2 *>(&xbb);
         __half2 r[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) r[q] = __hadd2(pa[q], pb[q]);  // correctly rounded
         xa = *reinterpret_cast<uint4 *>(r);
         *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
-      } else if (gather) {
+      } else if (SRC == 3) {
         *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
       }
       v[c] = xa;
@@ -147,25 +160,40 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   if (nchunk > 4096) return hipErrorInvalidValue;
   const float *pp = x2p.S > 0 ? x2p.p : nullptr;
   if (pp && x2p.S > 8) return hipErrorInvalidValue;
+  if ((x2 || pp) && !res_out) return hipErrorInvalidValue;
+  // split-K slabs: one 8-column chunk per thread (H <= 8192); the model does
+  // not defer its o/down partials beyond that
+  if (pp && nchunk > 1024) return hipErrorInvalidValue;
+  const int src = gather ? 3 : pp ? 2 : x2 ? 1 : 0;
   const int ms = !pp || x2p.S <= 1 ? 1 : x2p.S <= 2 ? 2 : x2p.S <= 4 ? 4 : 8;
-#define FFMI_RMS2(NT, MC, MS)                                                                   \
-  hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS>), dim3(T), dim3(NT), 0, s, x1, x2, w, res_out, \
-                     out, H, eps, op, pp, x2p.S, x2p.NP, gather)
+#define FFMI_RMS3(NT, MC, MS, SR)                                                              \
+  hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS, SR>), dim3(T), dim3(NT), 0, s, x1, x2, w,    \
+                     res_out, out, H, eps, op, pp, x2p.S, x2p.NP, gather)
 #define FFMI_RMS(NT, MC)                                   \
   do {                                                     \
-    if (ms == 1) FFMI_RMS2(NT, MC, 1);                     \
-    else if (ms == 2) FFMI_RMS2(NT, MC, 2);                \
-    else if (ms == 4) FFMI_RMS2(NT, MC, 4);                \
-    else FFMI_RMS2(NT, MC, 8);                             \
+    if (src == 0) FFMI_RMS3(NT, MC, 1, 0);                 \
+    else if (src == 1) FFMI_RMS3(NT, MC, 1, 1);            \
+    else if (src == 3) FFMI_RMS3(NT, MC, 1, 3);            \
+    else if (ms == 1) FFMI_RMS3(NT, MC, 1, 2);             \
+    else if (ms == 2) FFMI_RMS3(NT, MC, 2, 2);             \
+    else if (ms == 4) FFMI_RMS3(NT, MC, 4, 2);             \
+    else FFMI_RMS3(NT, MC, 8, 2);                          \
+  } while (0)
+#define FFMI_RMS_NOSLAB(NT, MC)                            \
+  do {                                                     \
+    if (src == 0) FFMI_RMS3(NT, MC, 1, 0);                 \
+    else if (src == 1) FFMI_RMS3(NT, MC, 1, 1);            \
+    else FFMI_RMS3(NT, MC, 1, 3);                          \
   } while (0)
   if (nchunk <= 128) FFMI_RMS(128, 1);
   else if (nchunk <= 256) FFMI_RMS(256, 1);
   else if (nchunk <= 512) FFMI_RMS(512, 1);
   else if (nchunk <= 1024) FFMI_RMS(1024, 1);
-  else if (nchunk <= 2048) FFMI_RMS(1024, 2);
-  else FFMI_RMS(1024, 4);
+  else if (nchunk <= 2048) FFMI_RMS_NOSLAB(1024, 2);
+  else FFMI_RMS_NOSLAB(1024, 4);
+#undef FFMI_RMS_NOSLAB
 #undef FFMI_RMS
-#undef FFMI_RMS2
+#undef FFMI_RMS3
   return hipGetLastError();
 }
 

@@ -463,7 +463,7 @@ struct LlamaGPU : public ffmi_model {
       pr = prof_begin(on);
       ffmi::Partials o_part;
       FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
-                                 o.tp_size == 1 ? &o_part : nullptr));
+                                 o.tp_size == 1 && H <= 8192 ? &o_part : nullptr));
       prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));
@@ -478,7 +478,7 @@ struct LlamaGPU : public ffmi_model {
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       pr = prof_begin(on);
       FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
-                                 o.tp_size == 1 ? &down_part : nullptr));
+                                 o.tp_size == 1 && H <= 8192 ? &down_part : nullptr));
       prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
       pr = prof_begin(on && o.tp_size > 1);
       TRY(allreduce(proj, (size_t)T * H));

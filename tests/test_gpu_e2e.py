@@ -28,8 +28,9 @@ def prompts(n, V, lo, hi, seed):
     return [rng.integers(3, V, size=int(rng.integers(lo, hi))).tolist() for _ in range(n)]
 
 
-def check_tokens_vs_oracle(cfg, seed, seq, n_prompt):
-    """teacher-forced check of seq[n_prompt:] against the oracle."""
+def check_tokens_vs_oracle(cfg, seed, seq, n_prompt, tie_ulp=2):
+    """teacher-forced check of seq[n_prompt:] against the oracle; a mismatch
+    must be a tie within tie_ulp fp16 ulp of the two tokens' probabilities."""
     m = O.Model(cfg, seed, fp16=1, max_requests=1, max_seq=len(seq) + 1)
     logits = m.forward(0, np.array(seq[:-1], np.int32), 0)
     gen = seq[n_prompt:]
@@ -43,7 +44,8 @@ def check_tokens_vs_oracle(cfg, seed, seq, n_prompt):
         row = lg[t]
         p = np.exp(row - row.max())
         p16 = (p / p.sum()).astype(np.float16)
-        assert ulp_diff(p16[g], p16[ids[t]]) <= 2, (t, g, ids[t], float(p16[g]), float(p16[ids[t]]))
+        assert ulp_diff(p16[g], p16[ids[t]]) <= tie_ulp, (t, g, ids[t], float(p16[g]),
+                                                          float(p16[ids[t]]))
     assert exact >= 0.9 * len(gen), (exact, len(gen))
     return exact
 

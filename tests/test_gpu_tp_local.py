@@ -8,8 +8,10 @@ in-process shard group (ffmi_comm_create_local): the same sharded weights
 (model.cc:3421-3445) and the same replicated norms / lm_head / SSM as a
 one-process-per-GPU run, only the sum is done by a group kernel instead of
 RCCL.  Every rank must emit identical tokens, and those must be oracle-valid
-greedy sequences of the UNSHARDED model (exact picks or 2-ulp ties, >= 90 %
-exact: the partial sums are rounded to fp16 before the all-reduce).
+greedy sequences of the UNSHARDED model: >= 90 % exact picks, every other pick
+a tie within 2*TP fp16 ulp (each of the TP row-parallel partial sums is
+rounded to fp16 before the all-reduce, so the logits carry up to TP extra
+roundings per layer against the unsharded fp32-accumulated GEMM).
 """
 import threading
 
@@ -74,7 +76,7 @@ def test_tp_shards_decode_like_unsharded_model(cfg, tp):
         assert [x.output_tokens for x in res[r]] == [x.output_tokens for x in res[0]]
     for p, x in zip(ps, res[0]):
         assert len(x.output_tokens) == 56
-        check_tokens_vs_oracle(cfg, 11, x.output_tokens, len(p) + 1)
+        check_tokens_vs_oracle(cfg, 11, x.output_tokens, len(p) + 1, tie_ulp=2 * tp)
 
 
 def test_tp2_spec_infer_tokens_are_greedy():
@@ -82,4 +84,4 @@ def test_tp2_spec_infer_tokens_are_greedy():
     res = run_tp(LLM_CFG, 11, 2, ps, 60, spec=True)
     assert [x.output_tokens for x in res[1]] == [x.output_tokens for x in res[0]]
     for p, x in zip(ps, res[0]):
-        check_tokens_vs_oracle(LLM_CFG, 11, x.output_tokens, len(p) + 1)
+        check_tokens_vs_oracle(LLM_CFG, 11, x.output_tokens, len(p) + 1, tie_ulp=4)
