@@ -647,9 +647,12 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   double best = 1e30;
   p.NTW = 8, p.S = 1;
   // measured k-step times (us) at MTW = 3, packed activations (diag_stamps.py)
-  static const int ntw_opts[4] = {6, 8, 12, 16};
-  static const double base[4] = {0.36, 0.40, 0.65, 0.90};
-  for (int o = 0; o < 4; ++o) {
+  // (2 and 4: narrow per-rank shards of tensor parallelism, e.g. LLaMA-7B
+  // o_proj at TP = 8 is 256 tiles x K = 512 -- 43 workgroups at NTW = 6)
+  static const int ntw_opts[6] = {2, 4, 6, 8, 12, 16};
+  static const double base[6] = {0.27, 0.30, 0.36, 0.40, 0.65, 0.90};
+  static const int nopt = getenv("FFMI_MID_NARROW") && atoi(getenv("FFMI_MID_NARROW")) == 0 ? 4 : 6;
+  for (int o = 6 - nopt; o < 6; ++o) {
     const int ntw = ntw_opts[o];
     const int nblk = (ntiles + ntw - 1) / ntw;
     for (int S = 1; S <= 8 && S <= KT; ++S) {
@@ -673,7 +676,8 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       const int n = sscanf(q, "%d:%d:%d,%d", &a, &b, &c, &d);
       if (n == 4 && a == N && b == K) ntw = c, S = d;
       else if (n != 4 && sscanf(q, "%d,%d", &a, &b) == 2) ntw = a, S = b;
-      if ((ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) && S >= 1 && S <= std::min(KT, 8)) {
+      if ((ntw == 2 || ntw == 4 || ntw == 6 || ntw == 8 || ntw == 12 || ntw == 16) && S >= 1 &&
+          S <= std::min(KT, 8)) {
         p.NTW = ntw, p.S = S;
         break;
       }
@@ -779,11 +783,15 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
 #define FFMI_RUN(M, NW) \
   return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer)
     if (p.MTW == 3) {
+      if (p.NTW == 2) FFMI_RUN(3, 2);
+      if (p.NTW == 4) FFMI_RUN(3, 4);
       if (p.NTW == 16) FFMI_RUN(3, 16);
       if (p.NTW == 12) FFMI_RUN(3, 12);
       if (p.NTW == 6) FFMI_RUN(3, 6);
       FFMI_RUN(3, 8);
     }
+    if (p.NTW == 2) FFMI_RUN(2, 2);
+    if (p.NTW == 4) FFMI_RUN(2, 4);
     if (p.NTW == 16) FFMI_RUN(2, 16);
     if (p.NTW == 12) FFMI_RUN(2, 12);
     if (p.NTW == 6) FFMI_RUN(2, 6);
