@@ -1,0 +1,14 @@
+#!/bin/bash
+# Bench-only A/B of environment settings: scripts/gpu_env_bench_ab.sh "VAR=a" "VAR=b" ...
+set -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"; mkdir -p gpurun_out
+for P in "$@"; do
+  echo "== $P"
+  env $P timeout -k 10 300 python bench.py --no-cpu-baseline --steps 2 > gpurun_out/eb.json 2>gpurun_out/eb.err || { tail -3 gpurun_out/eb.err; exit 1; }
+  python3 -c "
+import json
+for l in open('gpurun_out/eb.json'):
+    if l.startswith('{'):
+        d=json.loads(l); print(d['value'], d['time_split_ms_per_generate'], d['incr_decoding']['value'])"
+done
