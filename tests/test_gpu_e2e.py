@@ -174,3 +174,55 @@ def test_spec_infer_equals_incr_on_gpu(ssm):
             assert first_divergence(a.output_tokens, b.output_tokens) == len(a.output_tokens)
     if ssm == "same":
         assert s_inc.llm_steps >= 1.5 * s_spec.llm_steps  # cpp_inference_tests.sh:191-201
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_sequences_run_to_max_sequence_length(spec):
+    """Requests that grow to max_sequence_length - 1 tokens (the reference's
+    limit, request_manager.cc:386-391): the last KV slots and, for SpecInfer,
+    the tree slots past them stay in bounds; tokens stay oracle-valid."""
+    S = 64
+    ps = prompts(3, LLM_CFG["vocab_size"], 5, 12, 23)
+    kw = dict(max_requests_per_batch=4, max_tokens_per_batch=32, max_sequence_length=S)
+    if spec:
+        llm = fa.Model(LLM_CFG, "tree", max_requests=4, max_tokens=32 + 23 * 4, max_seq_len=S,
+                       max_tree_tokens=23, weight_seed=11)
+        ssm = fa.Model(SSM_CFG, "beam", max_requests=4, max_tokens=32 + 23 * 4, max_seq_len=S,
+                       max_tree_tokens=23, weight_seed=5)
+        rm = fa.RequestManager(spec_tree_width=(1, 1, 3), max_spec_tree_token_num=23, **kw)
+        rm.register_ssm_model(ssm)
+    else:
+        llm = fa.Model(LLM_CFG, "inc", max_requests=4, max_tokens=32, max_seq_len=S,
+                       weight_seed=11)
+        rm = fa.RequestManager(**kw)
+    res = fa.generate(rm, llm, ps, max_length=S - 1, spec=spec)
+    for p, r in zip(ps, res):
+        assert len(r.output_tokens) == S - 1
+        check_tokens_vs_oracle(LLM_CFG, 11, r.output_tokens, len(p) + 1)
+
+
+def test_single_request_and_queued_requests():
+    """Batch of one (T = 1 decode steps) and more requests than batch slots
+    (continuous batching admits queued requests as slots free up,
+    request_manager.cc:713-1135): every request completes with greedy tokens
+    equal to its solo run."""
+    ps = prompts(9, LLM_CFG["vocab_size"], 3, 25, 29)
+    kw = dict(max_tokens_per_batch=16, max_sequence_length=128)
+    solo = []
+    for p in ps[:3]:
+        llm = fa.Model(LLM_CFG, "inc", max_requests=1, max_tokens=16, max_seq_len=128,
+                       weight_seed=11)
+        r = fa.generate(fa.RequestManager(max_requests_per_batch=1, **kw), llm, [p],
+                        max_length=48)[0]
+        check_tokens_vs_oracle(LLM_CFG, 11, r.output_tokens, len(p) + 1)
+        solo.append(r.output_tokens)
+    llm = fa.Model(LLM_CFG, "inc", max_requests=4, max_tokens=16, max_seq_len=128,
+                   weight_seed=11)
+    res = fa.generate(fa.RequestManager(max_requests_per_batch=4, **kw), llm, ps, max_length=48)
+    assert all(len(r.output_tokens) == 48 for r in res)
+    for p, r in zip(ps, res):
+        check_tokens_vs_oracle(LLM_CFG, 11, r.output_tokens, len(p) + 1)
+    # batching changes nothing but fp32 summation order: equal or oracle-valid ties
+    for a, r in zip(solo, res[:3]):
+        if a != r.output_tokens:
+            assert first_divergence(a, r.output_tokens) > 0
