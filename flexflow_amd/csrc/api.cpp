@@ -395,7 +395,7 @@ extern "C" ffmi_status ffmi_linear_ws(const void *X, const void *W_packed, void 
                                       size_t workspace_bytes, ffmi_stream stream) {
   FFMI_CHECK(X && W_packed && Y && T >= 0 && out_dim > 0, FFMI_ERR_INVALID);
   FFMI_CHECK(in_dim > 0 && in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
-  const int epi = epilogue & ~FFMI_X_PACKED;
+  const int epi = epilogue & ~(FFMI_X_PACKED | FFMI_W_STREAM);
   const int epi_base = epi & ~FFMI_Y_PACKED;
   FFMI_CHECK(epi_base == FFMI_EPI_NONE || epi_base == FFMI_EPI_SILU_MUL, FFMI_ERR_INVALID);
   FFMI_CHECK(!(epilogue & FFMI_Y_PACKED) || out_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);

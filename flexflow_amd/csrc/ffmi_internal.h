@@ -31,6 +31,18 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
 
+// Weight fragment load.  NT (FFMI_W_STREAM launches: a model whose weights
+// exceed the Infinity Cache, each weight byte read by one workgroup) puts the
+// non-temporal hint on the load (MI355X_MICROARCH.md "nt-weights"), so the
+// stream does not evict the KV cache, activations or the SSM's weights from
+// L2 / the Infinity Cache.  A model that fits (the 68M SSM, replayed step
+// after step) keeps the default policy.
+template <bool NT>
+__device__ __forceinline__ h8 ld_weight(const uint16_t *p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const h8 *>(p));
+  else return *reinterpret_cast<const h8 *>(p);
+}
+
 // Packed activation tiles (FFMI_X_PACKED / FFMI_Y_PACKED): element (m, n) of a
 // [T][K] activation lives at [m/16][n/32][lane = (m&15) + 16*((n>>3)&3)][n&7],
 // i.e. each 16-row x 32-column block is one MFMA operand fragment (1 KiB,

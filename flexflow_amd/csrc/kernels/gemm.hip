@@ -58,7 +58,7 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
 // workgroup reduces its K slice over its waves and writes an fp32 partial
 // slab [S][T][NTILES*16] that the consumer combines in slice order
 // (Partials, the M-split kernel's slab layout).
-template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false>
+template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false, bool NTL = false>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         for (int u = 0; u < UP; ++u)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            bb[u][j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)(k0 + u) * 512);
+            bb[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(k0 + u) * 512);
 #pragma unroll
         for (int u = 0; u < UP; ++u)
 #pragma unroll
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        b[u][j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)(kt + u) * 512);
+        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(kt + u) * 512);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
       const int kk = min(kt + u, ke - 1);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        b[u][j] = *reinterpret_cast<const h8 *>(wrow[j] + (size_t)kk * 512);
+        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)kk * 512);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
@@ -294,7 +294,8 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 
 template <int MT, int NT, int KW, int U, int EPI>
 static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws, int T,
-                      int N, int K, int KT, int NTILES, int S, hipStream_t s, int xp, int yp) {
+                      int N, int K, int KT, int NTILES, int S, hipStream_t s, int xp, int yp,
+                      bool nt) {
   const int ncb = (NTILES + NT - 1) / NT;
   dim3 grid(ncb, S);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
@@ -306,12 +307,17 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
   static const int force = getenv("FFMI_SKINNY_PIPE") ? atoi(getenv("FFMI_SKINNY_PIPE")) : -1;
   const int per_wave = ((KT + S - 1) / S + KW - 1) / KW;
   const bool pipe = force >= 0 ? force != 0 : per_wave >= 2 * U;
-  if (pipe)
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, true>), grid, dim3(KW * 64), lds, s,
-                       X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
-  else
-    hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI>), grid, dim3(KW * 64), lds, s, X,
-                       Wp, Y, ws, T, N, K, KT, NTILES, xp, yp);
+#define FFMI_SKINNY_LAUNCH(PP, NL)                                                             \
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, PP, NL>), grid, dim3(KW * 64), lds, \
+                     s, X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp)
+  if (pipe) {
+    if (nt) FFMI_SKINNY_LAUNCH(true, true);
+    else FFMI_SKINNY_LAUNCH(true, false);
+  } else {
+    if (nt) FFMI_SKINNY_LAUNCH(false, true);
+    else FFMI_SKINNY_LAUNCH(false, false);
+  }
+#undef FFMI_SKINNY_LAUNCH
   return hipGetLastError();
 }
 
@@ -331,10 +337,10 @@ static int skinny_split(int T, int N, int K, int epi, bool deferrable) {
 template <int MT, int U>
 static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                               int T, int N, int K, int KT, int epi, int S, hipStream_t s,
-                              int xp = 0, int yp = 0) {
+                              int xp, int yp, bool nt) {
   int ntiles = (N + 15) / 16;
   if (epi == FFMI_EPI_SILU_MUL)
-    return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp);
+    return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt);
   // diagnostics: FFMI_SKINNY="NT,KW" forces the tile count and K-split waves
   // of every unsplit skinny launch (A/B runs, scripts/gemm_bench.py)
   static int fnt = -1, fkw = 0;
@@ -343,27 +349,27 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
     if (const char *e = getenv("FFMI_SKINNY")) (void)sscanf(e, "%d,%d", &fnt, &fkw);
   }
   if (fnt > 0 && S == 1 && MT <= 2) {
-    if (fnt == 1 && fkw == 4) return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 1 && fkw == 8) return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 2 && fkw == 4) return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 2 && fkw == 8) return run<MT, 2, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
-    if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp);
+    if (fnt == 1 && fkw == 4) return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 1 && fkw == 8) return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 2 && fkw == 4) return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 2 && fkw == 8) return run<MT, 2, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
   }
   // wide layers (lm_head): two tiles per workgroup once there are >= 2 row
   // tiles (SSM lm_head at T = 24: 16.1 -> 12.3 us warm; at one row tile a
   // single tile stays faster: LLaMA-7B lm_head T = 8 cold 47.8 vs 55.8 us)
   if (MT >= 2 && ntiles >= 512)
-    return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+    return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
   // 8-wave groups only where the accumulators fit 2 waves/SIMD (no spills)
   if (ntiles >= 512 || MT >= 8)
-    return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+    return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
   // ... and where each wave still gets a full batch of U k-steps (K = 768 of
   // the SSM: 4 waves x 6 k-steps beat 8 x 3, qkv T = 24: 5.7 -> 4.2 us)
   if ((KT + S - 1) / S >= 8 * U)
-    return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
-  return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp);
+    return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
+  return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
 }
 
 // ---------------------------------------------------------------------------
@@ -442,7 +448,8 @@ __device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *_
 __device__ long long *g_gemm_stamps;
 __device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 
-template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false, bool ULD = false>
+template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false, bool ULD = false,
+          bool NTL = false>
 __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
@@ -512,7 +519,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kq * 512);
     }
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
@@ -538,7 +545,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kw * 512);
       // B(kt+1) lives in ring slot (Q+1) % PF
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
@@ -690,7 +697,7 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
 }
 
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
-  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
+  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED | FFMI_W_STREAM);
   const int mtiles = (T + 15) / 16;
   if (mtiles <= 4) {
     const int S = skinny_split(T, N, K, epilogue, true);
@@ -705,7 +712,7 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
 template <int MTW, int NTW, int PF>
 static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s,
-                          bool xpacked, int yp, int S, Partials *defer) {
+                          bool xpacked, int yp, int S, Partials *defer, bool nt) {
   const int KT = K / 32;
   const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
   const int mtiles = (T + 15) / 16;
@@ -719,14 +726,20 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   // 55.9 -> 51.2 us, qkv 37.2 -> 34.6 us in scripts/gemm_bench.py);
   // FFMI_MID_ULD=0 turns them off (A/B runs)
   static const bool uld = !getenv("FFMI_MID_ULD") || atoi(getenv("FFMI_MID_ULD")) != 0;
-#define FFMI_MID(E, ST, XPK)                                                                      \
-  do {                                                                                            \
-    if (uld && NTW % 4)                                                                           \
-      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK, true>), grid, dim3(256), 0, s, \
-                         X, Wp, Y, ws, T, N, K, KT, ntiles, S, yp);                               \
-    else                                                                                          \
-      hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK>), grid, dim3(256), 0, s, X,   \
-                         Wp, Y, ws, T, N, K, KT, ntiles, S, yp);                                  \
+  // non-temporal weight loads only where each weight tile has ONE reader
+  // (mblocks == 1); prefill blocks re-read every tile from L2 / the MALL
+  const bool ntl = nt && mblocks == 1;
+#define FFMI_MID2(E, ST, XPK, U, NL)                                                               \
+  hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK, U, NL>), grid, dim3(256), 0, s, X, \
+                     Wp, Y, ws, T, N, K, KT, ntiles, S, yp)
+#define FFMI_MID(E, ST, XPK)                                  \
+  do {                                                        \
+    const bool u_ = uld && NTW % 4;                           \
+    if (ST) FFMI_MID2(E, ST, XPK, false, false);              \
+    else if (u_ && ntl) FFMI_MID2(E, false, XPK, true, true); \
+    else if (u_) FFMI_MID2(E, false, XPK, true, false);       \
+    else if (ntl) FFMI_MID2(E, false, XPK, false, true);      \
+    else FFMI_MID2(E, false, XPK, false, false);              \
   } while (0)
   if (stamp && !epi && stamp_buf()) {
     g_stamp_entries = (long)nblk * S * mblocks * 4;
@@ -740,6 +753,7 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
     else FFMI_MID(0, false, false);
   }
 #undef FFMI_MID
+#undef FFMI_MID2
   if (defer) {
     defer->S = 0;
     if (S > 1 && !epi) {  // the consumer combines the slabs
@@ -776,12 +790,13 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   const int mtiles = (T + 15) / 16;
   const bool xp = (epilogue & FFMI_X_PACKED) != 0;
   const int yp = (epilogue & FFMI_Y_PACKED) ? 1 : 0;
-  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED);
+  const bool nt = (epilogue & FFMI_W_STREAM) != 0;
+  epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED | FFMI_W_STREAM);
   if ((xp && K % 32) || (yp && N % 32)) return hipErrorInvalidValue;
   if (mtiles > 4) {
     const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);
 #define FFMI_RUN(M, NW) \
-  return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer)
+  return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer, nt)
     if (p.MTW == 3) {
       if (p.NTW == 2) FFMI_RUN(3, 2);
       if (p.NTW == 4) FFMI_RUN(3, 4);
@@ -803,9 +818,9 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   const size_t need = (size_t)S * T * ((N + 15) / 16) * 16 * sizeof(float);
   if (S > 1 && (!ws || ws_bytes < need)) S = 1;
   hipError_t e;
-  if (mtiles <= 1) e = dispatch_nt<1, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
-  else if (mtiles <= 2) e = dispatch_nt<2, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
-  else e = dispatch_nt<4, 4>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp);
+  if (mtiles <= 1) e = dispatch_nt<1, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
+  else if (mtiles <= 2) e = dispatch_nt<2, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
+  else e = dispatch_nt<4, 4>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
   if (S > 1 && e == hipSuccess) defer->p = ws, defer->S = S, defer->NP = (N + 15) / 16 * 16;
   return e;
 }

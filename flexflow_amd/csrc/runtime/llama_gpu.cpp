@@ -42,6 +42,10 @@ struct LlamaGPU : public ffmi_model {
   // packed activation tiles: every GEMM then reads its activation fragments
   // as contiguous 1 KiB blocks, like the weights (see act_packed_off)
   bool packed = false;
+  // FFMI_W_STREAM on every GEMM when this rank's weights outgrow the 256 MiB
+  // Infinity Cache (LLaMA-7B: 13.5 GB streamed once per step; the 68M SSM's
+  // 87 MB stay cached from step to step and keep the default policy)
+  int wstream = 0;
   hipStream_t stream = nullptr;
   std::vector<Layer> layers;
   uint16_t *embed = nullptr, *final_norm = nullptr, *lm = nullptr;
@@ -241,6 +245,13 @@ struct LlamaGPU : public ffmi_model {
     FFMI_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
     const int Tm = (o.max_tokens + 15) & ~15;  // packed tiles cover 16-row groups
     packed = H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0;
+    {
+      const double wbytes = 2.0 * c.num_layers * ((double)4 * Hl * H + 3.0 * Fl * H) +
+                            2.0 * V * H;
+      wstream = wbytes > 192.0 * (1 << 20) ? FFMI_W_STREAM : 0;
+      if (const char *e = getenv("FFMI_W_STREAM"))  // A/B override: 0 / 1
+        wstream = atoi(e) ? FFMI_W_STREAM : 0;
+    }
     ffmi_status st;
 #define TRY(x) \
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
@@ -443,7 +454,7 @@ struct LlamaGPU : public ffmi_model {
       // split-K GEMMs leave their partial slabs for the next kernel to combine
       // (rope-store for qkv; the residual norm for o/down when there is no
       // all-reduce in between) instead of a separate reduce pass
-      const int XP = packed ? FFMI_X_PACKED : 0;
+      const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
       // layer 0: the embedding lookup gathers straight into the first norm
       // (embedding_kernels.cu:233-244; res = the looked-up rows)
       FFMI_HIP(ffmi::launch_rmsnorm(l == 0 ? embed : res, l == 0 ? nullptr : proj, L.in_norm, res,
@@ -484,7 +495,7 @@ struct LlamaGPU : public ffmi_model {
       TRY(allreduce(proj, (size_t)T * H));
       prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
     }
-    const int XP = packed ? FFMI_X_PACKED : 0;
+    const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
     pr = prof_begin(ptail);
     FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
                                   down_part));

@@ -7,7 +7,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libffmi.so")
+# FFMI_LIB_VARIANT=<suffix> loads libffmi_<suffix>.so from the same directory
+# (build-flag A/B runs, e.g. scripts/gpu_lib_ab.sh); the default is libffmi.so
+_VARIANT = os.environ.get("FFMI_LIB_VARIANT", "")
+LIB_PATH = os.path.join(_HERE, f"libffmi_{_VARIANT}.so" if _VARIANT else "libffmi.so")
 
 c_int, c_float, c_void_p, c_size_t, c_uint64, c_int64, c_double, c_long = (
     ctypes.c_int, ctypes.c_float, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64,
@@ -21,6 +24,7 @@ MODEL_INC, MODEL_BEAM, MODEL_TREE = 0, 1, 2
 EPI_NONE, EPI_SILU_MUL = 0, 1
 X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
 Y_PACKED = 0x20  # FFMI_Y_PACKED
+W_STREAM = 0x40  # FFMI_W_STREAM: non-temporal weight loads (speed only)
 F16, F32, I32 = 0, 1, 2
 ATTN_QTILE = 32
 MAX_TREE = 64

@@ -164,6 +164,11 @@ typedef enum {
 /* OR into `epilogue`: write Y in packed activation tiles (a GEMM input of the
  * next layer; out_dim % 32 == 0). */
 #define FFMI_Y_PACKED 0x20
+/* OR into `epilogue`: the weights are a once-read stream (a model larger than
+ * the 256 MiB Infinity Cache): their loads carry the non-temporal hint so they
+ * do not evict the KV cache, activations or a small model's weights.  Speed
+ * only; results are identical. */
+#define FFMI_W_STREAM 0x40
 size_t ffmi_packed_activation_bytes(int T, int in_dim);
 ffmi_status ffmi_pack_activations(const void *X, int T, int in_dim, void *X_packed,
                                   ffmi_stream stream);

@@ -566,3 +566,26 @@ def test_allreduce_single_rank_and_silu():
     gb, ub, ob = Buf(g), Buf(u), Buf.empty((5000,), np.float16)
     F.check(L.ffmi_silu_mul(gb.ptr, ub.ptr, ob.ptr, 5000, None))
     close16(ob.get(), O.silu_mul(g.astype(np.float32), u.astype(np.float32)), 1, 0.995)
+
+
+@pytest.mark.parametrize("T", [1, 8, 24, 64, 168, 300])
+@pytest.mark.parametrize("epi", [0, 1])
+def test_linear_weight_stream_hint_bit_identical(T, epi):
+    """FFMI_W_STREAM (non-temporal weight loads) changes the cache policy
+    only: skinny, M-split (one and several row blocks) and split-K paths give
+    the same bits as the default policy."""
+    rng = np.random.default_rng(2000 + T + epi)
+    N, K = 1024, 2048
+    X = f16(rng.standard_normal((T, K)))
+    if epi:
+        Wg, Wu = f16(rng.uniform(-0.05, 0.05, (N, K))), f16(rng.uniform(-0.05, 0.05, (N, K)))
+        gb, ub = Buf(Wg), Buf(Wu)
+        Wp = Buf.empty((2 * L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+    else:
+        Wp = packed(f16(rng.uniform(-0.05, 0.05, (N, K))))
+    Xb = Buf(X)
+    Y0, Y1 = Buf.empty((T, N), np.float16), Buf.empty((T, N), np.float16)
+    F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y0.ptr, T, N, K, epi, None))
+    F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y1.ptr, T, N, K, epi | F.W_STREAM, None))
+    assert np.array_equal(Y0.get().view(np.uint16), Y1.get().view(np.uint16))
