@@ -76,6 +76,19 @@ extern "C" ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm) {
   return FFMI_OK;
 }
 
+extern "C" ffmi_status ffmi_rm_register_output_filepath(ffmi_rm *rm, const char *path) {
+  if (!rm) return FFMI_ERR_INVALID;
+  rm->rm.register_output_filepath(path ? path : "");
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rm_register_detokenizer(ffmi_rm *rm, ffmi_detokenize_fn fn,
+                                                    void *ctx) {
+  if (!rm) return FFMI_ERR_INVALID;
+  rm->rm.register_detokenizer(fn, ctx);
+  return FFMI_OK;
+}
+
 extern "C" int64_t ffmi_rm_register_request(ffmi_rm *rm, const int *prompt, int n_prompt,
                                             int max_length, int max_new_tokens,
                                             int add_special_tokens) {

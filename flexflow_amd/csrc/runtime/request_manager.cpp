@@ -117,7 +117,7 @@ bool RequestManager::check_inf_req_completion(const BatchConfig &old_bc, int i) 
   return is_eos_token(request.tokens.back());
 }
 
-void RequestManager::complete_request(Request &request) {
+void RequestManager::complete_request(Request &request, bool spec) {
   request.status = Request::COMPLETED;
   GenerationResult &gr = request_generation_results[request.guid];
   gr.output_tokens = request.tokens;
@@ -128,6 +128,42 @@ void RequestManager::complete_request(Request &request) {
     printf("[ffmi] guid(%lld) done: len %zu llm_steps %d latency %.1f us\n",
            (long long)request.guid, request.tokens.size(), pi.llm_decoding_steps,
            pi.finish_time - pi.start_time);
+  if (!output_filepath.empty()) write_output_record(request, spec);
+}
+
+std::string RequestManager::decode(const std::vector<int> &ids) const {
+  if (!detok) return std::string();
+  const int n = detok(ids.data(), (int)ids.size(), nullptr, 0, detok_ctx);
+  if (n <= 0) return std::string();
+  std::string out((size_t)n, '\0');
+  const int m = detok(ids.data(), (int)ids.size(), &out[0], n, detok_ctx);
+  out.resize((size_t)std::max(0, std::min(m, n)));
+  return out;
+}
+
+// The reference's per-request output record, appended on completion:
+// incremental decoding request_manager.cc:813-840 ("[Profile] guid(..)
+// llm_decoding_steps(..) latency(..) ttft(..)"), SpecInfer :1303-1330 (no
+// ttft); then "token IDs: a,b,...", a newline and the decoded text, which the
+// reference writes without a trailing newline.  Times in microseconds with 3
+// decimals.  Warmup requests do not exist here, so the tag is always Profile.
+void RequestManager::write_output_record(const Request &request, bool spec) const {
+  FILE *f = fopen(output_filepath.c_str(), "a");
+  if (!f) {
+    fprintf(stderr, "Unable to open the output file: %s\n", output_filepath.c_str());
+    return;
+  }
+  const ProfileInfo &pi = profiling_requests.at(request.guid);
+  fprintf(f, "[Profile] guid(%lld) llm_decoding_steps(%d) latency(%.3f)", (long long)request.guid,
+          pi.llm_decoding_steps, pi.finish_time - pi.start_time);
+  if (!spec) fprintf(f, " ttft(%.3f)", pi.first_token_time - pi.registration_time);
+  fputs("\ntoken IDs: ", f);
+  for (size_t i = 0; i < request.tokens.size(); ++i)
+    fprintf(f, i + 1 < request.tokens.size() ? "%d," : "%d", request.tokens[i]);
+  fputc('\n', f);
+  const std::string text = decode(request.tokens);
+  fwrite(text.data(), 1, text.size(), f);
+  fclose(f);
 }
 
 // request_manager.cc:713-1135 (inference requests only)
@@ -264,7 +300,7 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
       if ((int)(verified_tokens.size() + request.tokens.size()) >= request.max_length) {
         for (const auto &tp : verified_tokens)
           if (tp.second < request.max_length) request.tokens.push_back(tp.first);
-        complete_request(request);
+        complete_request(request, true);
         new_bc.request_completed[i] = true;
         new_bc.request_running[i] = false;
         dfs_tree_inputs.erase(guid);

@@ -75,6 +75,14 @@ class RequestManager {
     return (int)ssm_models.size() - 1;
   }
   size_t get_num_ssms() const { return ssm_models.size(); }
+  // register_output_filepath (request_manager.cc:246-249): every completed
+  // request is appended to the file in the reference's record format
+  void register_output_filepath(const std::string &path) { output_filepath = path; }
+  // the reference's tokenizer_->Decode(request.tokens) (request_manager.cc:
+  // 786-789): a caller-supplied detokenizer (none: the text is empty)
+  typedef int (*Detokenizer)(const int *ids, int n, char *buf, int cap, void *ctx);
+  void register_detokenizer(Detokenizer fn, void *ctx) { detok = fn, detok_ctx = ctx; }
+  std::string decode(const std::vector<int> &ids) const;
   void set_verbose(bool v) { verbose = v; }
 
   RequestGuid register_new_request(const std::vector<int> &prompt, int max_length,
@@ -132,7 +140,8 @@ class RequestManager {
   } stats;
 
  private:
-  void complete_request(Request &request);
+  void complete_request(Request &request, bool spec = false);
+  void write_output_record(const Request &request, bool spec) const;
   void apply_limits() const;
 
   int max_requests_per_batch = 8;
@@ -143,6 +152,9 @@ class RequestManager {
   int bos_token_id = 1;
   std::vector<int> eos_token_ids;
   bool verbose = false;
+  std::string output_filepath;
+  Detokenizer detok = nullptr;
+  void *detok_ctx = nullptr;
 
   std::deque<Request> pending_infr_request_queue;
   std::map<RequestGuid, Request> all_requests;

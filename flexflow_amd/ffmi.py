@@ -151,6 +151,8 @@ SIGNATURES = {
     "ffmi_rm_create": (c_int, [ctypes.POINTER(RMConfig), ctypes.POINTER(c_void_p)]),
     "ffmi_rm_destroy": (None, [c_void_p]),
     "ffmi_rm_register_ssm": (c_int, [c_void_p, c_void_p]),
+    "ffmi_rm_register_output_filepath": (c_int, [c_void_p, ctypes.c_char_p]),
+    "ffmi_rm_register_detokenizer": (c_int, [c_void_p, c_void_p, c_void_p]),
     "ffmi_rm_register_request": (c_int64, [c_void_p, ctypes.POINTER(c_int), c_int, c_int, c_int,
                                            c_int]),
     "ffmi_rm_serve_incr_decoding": (c_int, [c_void_p, c_void_p]),
@@ -189,6 +191,11 @@ def lib():
             fn.argtypes = args
         _lib = L
     return _lib
+
+
+# ffmi_detokenize_fn: int (*)(const int *ids, int n, char *buf, int cap, void *ctx)
+DETOKENIZE_FN = ctypes.CFUNCTYPE(c_int, ctypes.POINTER(c_int), c_int, ctypes.c_void_p, c_int,
+                                 c_void_p)
 
 
 class FFMIError(RuntimeError):

@@ -142,6 +142,43 @@ class RequestManager:
         F.check(F.lib().ffmi_rm_register_ssm(self.handle, ssm.handle), "register ssm")
         self._ssms.append(ssm)
 
+    def register_output_filepath(self, path: Optional[str]):
+        """RequestManager::register_output_filepath (request_manager.cc:246-249):
+        completed requests are appended in the reference's record format."""
+        F.check(F.lib().ffmi_rm_register_output_filepath(
+            self.handle, path.encode() if path else None), "output filepath")
+
+    def register_tokenizer(self, tokenizer, bos_token_id=None, eos_token_ids=None):
+        """The text of each output record is tokenizer.decode(tokens), as the
+        reference's tokenizer_->Decode (request_manager.cc:786-789).  Any
+        object with decode(list[int]) -> str: a `tokenizers.Tokenizer`, an HF
+        tokenizer, or a test double.  BOS/EOS stay as configured at creation."""
+        if tokenizer is None:
+            self._detok = None
+            F.check(F.lib().ffmi_rm_register_detokenizer(self.handle, None, None), "detok")
+            return
+        cache = {}
+
+        def fn(ids, n, buf, cap, _ctx):
+            try:
+                key = tuple(ids[:n])
+                if buf is None or cap == 0:  # length query
+                    cache.clear()
+                    cache[key] = tokenizer.decode(list(key)).encode("utf-8")
+                    return len(cache[key])
+                data = cache.get(key)
+                if data is None:
+                    data = tokenizer.decode(list(key)).encode("utf-8")
+                m = min(cap, len(data))
+                ctypes.memmove(buf, data, m)
+                return m
+            except Exception:  # never unwind a Python error through C++
+                return 0
+
+        self._detok = F.DETOKENIZE_FN(fn)  # kept alive with the manager
+        F.check(F.lib().ffmi_rm_register_detokenizer(
+            self.handle, ctypes.cast(self._detok, ctypes.c_void_p), None), "detok")
+
     def register_new_request(self, prompt: List[int], max_length=-1, max_new_tokens=-1,
                              add_special_tokens=True) -> int:
         arr = F.int_array(list(prompt))

@@ -316,6 +316,16 @@ typedef struct {
 ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out);
 void ffmi_rm_destroy(ffmi_rm *rm);
 ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm);
+/* RequestManager::register_output_filepath (request_manager.cc:246-249):
+ * each completed request is appended in the reference's record format
+ * (incr decoding :813-840, SpecInfer :1303-1330).  NULL or "" turns it off. */
+ffmi_status ffmi_rm_register_output_filepath(ffmi_rm *rm, const char *path);
+/* The text written after "token IDs:" is the reference's
+ * tokenizer_->Decode(tokens) (request_manager.cc:786-789): the runtime calls
+ * fn(ids, n, NULL, 0, ctx) for the byte length, then fn(ids, n, buf, len, ctx).
+ * NULL fn: empty text (no tokenizer). */
+typedef int (*ffmi_detokenize_fn)(const int *ids, int n, char *buf, int cap, void *ctx);
+ffmi_status ffmi_rm_register_detokenizer(ffmi_rm *rm, ffmi_detokenize_fn fn, void *ctx);
 /* Request: prompt token ids (BOS is prepended when bos_token_id >= 0 and
  * add_special_tokens), max_length / max_new_tokens as in Request
  * (request_manager.cc:334-441).  Returns guid (> 0) or 0 on rejection. */
