@@ -74,6 +74,12 @@ struct LlamaGPU : public ffmi_model {
     double ms = 0, bytes = 0, flops = 0;
   };
   int prof_level = 0;
+  // level 1 samples every prof_every-th step (FFMI_PROF_EVERY, default 4):
+  // event-bracketed steps run eager, and bracketing every step cost the
+  // bench ~2.5 % of its tokens/s
+  int prof_every = getenv("FFMI_PROF_EVERY") ? std::max(1, atoi(getenv("FFMI_PROF_EVERY"))) : 4;
+  long prof_steps = 0;
+  bool prof_this_step = true;
   std::vector<hipEvent_t> ev_pool;
   size_t ev_used = 0;
   std::vector<ProfRec> recs;
@@ -89,7 +95,8 @@ struct LlamaGPU : public ffmi_model {
   }
   bool prof_on(int layer, int T) const {
     if (prof_level == 2) return true;
-    if (prof_level == 1) return T <= 256 && (layer == 0 || layer == c.num_layers / 2);
+    if (prof_level == 1)
+      return prof_this_step && T <= 256 && (layer == 0 || layer == c.num_layers / 2);
     return false;
   }
   int prof_begin(bool on) {
@@ -124,6 +131,7 @@ struct LlamaGPU : public ffmi_model {
   }
   ffmi_status set_profiling(int level) override {
     prof_level = level;
+    prof_steps = 0;
     for (auto &o : opstat) o = OpStat();
     return FFMI_OK;
   }
@@ -384,9 +392,12 @@ struct LlamaGPU : public ffmi_model {
   int tree_parity = 0;
   std::map<GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = getenv("FFMI_NO_GRAPHS") == nullptr;
+  // largest one-item-per-request step that is graphed (FFMI_GRAPH_MAXT: A/B)
+  int graph_max_t = getenv("FFMI_GRAPH_MAXT") ? atoi(getenv("FFMI_GRAPH_MAXT")) : 1024;
 
   ffmi_status forward(int k) {
     const int T = (int)ps.tokens.size();
+    prof_this_step = prof_level == 1 && (prof_steps++ % prof_every) == 0;
     ffmi_batch_desc desc;
     ps.desc(&desc);
     size_t bytes = 0;
@@ -394,8 +405,11 @@ struct LlamaGPU : public ffmi_model {
     if (st != FFMI_OK) return st;
     if (T == 0) return FFMI_OK;
     probs_h = reinterpret_cast<float *>(ids_h + (size_t)T * k);  // (also on graph replay)
-    const bool graph = use_graphs && T <= 64 && o.tp_size == 1 && !prof_on(0, T) &&
-                       !prof_on(c.num_layers / 2, T);
+    // graphed: small steps, and tree-verify steps of one work item per
+    // request (a fixed shape while the batch is full: T = 168 for 8 requests
+    // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
+    const bool graph = use_graphs && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
+                       o.tp_size == 1 && !prof_on(0, T) && !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
                          batch->commit_overlap ? 1 : 0, batch->one_item_per_req ? 1 : 0,

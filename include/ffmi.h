@@ -286,7 +286,9 @@ ffmi_status ffmi_model_create(const ffmi_llama_config *cfg, const ffmi_model_opt
 void ffmi_model_destroy(ffmi_model *m);
 /* Per-op device timing with HIP events on the model's stream (the
  * reference's --profiling, model.cc:4548-4550).  level 0: off; 1: sampled
- * (layers 0 and L/2, steps with <= 256 tokens); 2: every op of every step. */
+ * (layers 0 and L/2 of every 4th step with <= 256 tokens -- FFMI_PROF_EVERY
+ * sets the stride; sampled steps run eager, the others replay graphs);
+ * 2: every op of every step. */
 typedef struct {
   char name[32];
   long launches;

@@ -86,9 +86,13 @@ def test_long_prompts_exercise_split_k_paths():
     assert [r.output_tokens for r in spec] == [r.output_tokens for r in res]
 
 
-def test_graph_replay_equals_eager(monkeypatch):
-    """Small steps replay captured HIP graphs; FFMI_NO_GRAPHS=1 runs them
-    eagerly.  Same tokens either way, for incr decoding and SpecInfer."""
+@pytest.mark.parametrize("ssm", ["small", "same"])
+def test_graph_replay_equals_eager(monkeypatch, ssm):
+    """Small steps and tree-verify steps (one work item per request, T = 84
+    here) replay captured HIP graphs; FFMI_NO_GRAPHS=1 runs them eagerly.
+    Same tokens either way, for incr decoding and SpecInfer.  ssm="same"
+    (SSM == LLM weights) accepts long paths, so the verify graphs replay with
+    varying commit counts."""
     cfg, seed = LLM_CFG, 31
     ps = prompts(4, cfg["vocab_size"], 5, 40, seed)
     kw = dict(max_requests_per_batch=4, max_tokens_per_batch=64, max_sequence_length=128)
@@ -101,17 +105,20 @@ def test_graph_replay_equals_eager(monkeypatch):
                                                          max_length=80)]
         llm = fa.Model(cfg, "tree", max_requests=4, max_tokens=64 + 23 * 4, max_seq_len=128,
                        max_tree_tokens=23, weight_seed=seed)
-        ssm = fa.Model(SSM_CFG, "beam", max_requests=4, max_tokens=64 + 23 * 4, max_seq_len=128,
-                       max_tree_tokens=23, weight_seed=5)
+        small = ssm == "small"
+        draft = fa.Model(SSM_CFG if small else cfg, "beam", max_requests=4,
+                         max_tokens=64 + 23 * 4, max_seq_len=128, max_tree_tokens=23,
+                         weight_seed=5 if small else seed)
         rm = fa.RequestManager(spec_tree_width=(1, 1, 3), max_spec_tree_token_num=23, **kw)
-        rm.register_ssm_model(ssm)
+        rm.register_ssm_model(draft)
         return [r.output_tokens for r in fa.generate(rm, llm, ps, max_length=80, spec=True)]
 
     with_graphs = run(False), run(True)
     monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
     eager = run(False), run(True)
     assert with_graphs == eager
-    assert with_graphs[0] == with_graphs[1]  # SpecInfer == incr decoding
+    if ssm == "small":
+        assert with_graphs[0] == with_graphs[1]  # SpecInfer == incr decoding
 
 
 def test_incr_decoding_matches_golden_fixture_model():
