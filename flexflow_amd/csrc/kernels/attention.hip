@@ -83,10 +83,6 @@ hipError_t launch_commit(const char *blob, int C, const uint16_t *stage, uint16_
 //    otherwise (units past q_count load token 0 and store nothing);
 //  * V goes through LDS so that V^T rows are written as runs of consecutive
 //    slots instead of one 2-byte store per (token, d).
-__device__ __forceinline__ f4 ld_h4(const uint16_t *p) {
-  const uint2 r = *reinterpret_cast<const uint2 *>(p);
-  return f4{h2f(r.x & 0xffff), h2f(r.x >> 16), h2f(r.y & 0xffff), h2f(r.y >> 16)};
-}
 __device__ __forceinline__ f4 round_h4(f4 a) {  // fp16 value of the combined sum
   return f4{h2f(f2h(a[0])), h2f(f2h(a[1])), h2f(f2h(a[2])), h2f(f2h(a[3]))};
 }
@@ -112,17 +108,25 @@ __device__ __forceinline__ void kv_update_item(
   f4 x[U][6], y[U][6], cs[U][2];  // y: second fp32 slab
   int tslot[U], treq[U];  // (scalar fields: a struct copy would go to scratch)
   int tl[U], i0[U];
+  // One round trip for every prologue load.  The RoPE positions of the
+  // item's tokens come through the scalar cache (16 dwords of the work item,
+  // lgkmcnt), so the RoPE-row loads do not wait on any vector load; the qkv
+  // slabs (addresses known up front), the RoPE rows and the token records
+  // then go out back to back.  (Vector loads complete in issue order: with
+  // the positions loaded per lane, the RoPE rows waited for that load and
+  // for everything issued before it.)
+  const uint32_t *rp32 = reinterpret_cast<const uint32_t *>(wdp->rope_pos);
+  uint32_t rpw[FFMI_ATTN_QTILE / 2];
+#pragma unroll
+  for (int j = 0; j < FFMI_ATTN_QTILE / 2; ++j) rpw[j] = rp32[j];
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int e = min((int)threadIdx.x + u * NT, UNITS - 1);
     tl[u] = e / G, i0[u] = (e % G) * 4;
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
     const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
-    tslot[u] = bv.tokens[t].store_slot;
-    treq[u] = bv.tokens[t].req;
-    const int pos = min((int)wdp->rope_pos[tl[u] < w.q_count ? tl[u] : 0], max_rope_pos - 1);
-    const f4 *r = reinterpret_cast<const f4 *>(rope + ((size_t)pos * HD + i0[u]) * 2);
-    cs[u][0] = r[0];  // c0 s0 c1 s1
-    cs[u][1] = r[1];  // c2 s2 c3 s3
     const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
                         Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
                         2 * Hl + h * D + i0[u] + HD};
@@ -134,12 +138,40 @@ __device__ __forceinline__ void kv_update_item(
 #pragma unroll
       for (int c = 0; c < 6; ++c)
         y[u][c] = *reinterpret_cast<const f4 *>(p1 + (size_t)t * pNP + col[c]);
-    } else {
+    } else {  // raw fp16 bits now, converted after every load is out
 #pragma unroll
-      for (int c = 0; c < 6; ++c) x[u][c] = ld_h4(qkv + (size_t)t * 3 * Hl + col[c]);
+      for (int c = 0; c < 6; ++c) {
+        const uint2 r = *reinterpret_cast<const uint2 *>(qkv + (size_t)t * 3 * Hl + col[c]);
+        y[u][c] = f4{__uint_as_float(r.x), __uint_as_float(r.y), 0.f, 0.f};
+      }
     }
   }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int q = tl[u] < w.q_count ? tl[u] : 0;
+    uint32_t wd = rpw[0];
+#pragma unroll
+    for (int j = 1; j < FFMI_ATTN_QTILE / 2; ++j) wd = (q >> 1) == j ? rpw[j] : wd;
+    const int p = min((int)((q & 1) ? (wd >> 16) : (wd & 0xffffu)), max_rope_pos - 1);
+    const f4 *r = reinterpret_cast<const f4 *>(rope + ((size_t)p * HD + i0[u]) * 2);
+    cs[u][0] = r[0];  // c0 s0 c1 s1
+    cs[u][1] = r[1];  // c2 s2 c3 s3
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
+    tslot[u] = bv.tokens[t].store_slot;
+    treq[u] = bv.tokens[t].req;
+  }
   after_loads();
+  if (!part)
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int c = 0; c < 6; ++c) {
+        const uint32_t a = __float_as_uint(y[u][c][0]), b = __float_as_uint(y[u][c][1]);
+        x[u][c] = f4{h2f(a & 0xffff), h2f(a >> 16), h2f(b & 0xffff), h2f(b >> 16)};
+      }
   if (part) {  // slabs in slice order, then fp16 (partials_value)
     if (pS > 1)
 #pragma unroll
@@ -366,15 +398,15 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     }
   };
   // FUSED: a wave's first chunk lies below every slot this step writes for
-  // the request (host-computed `clean`): its loads go out before the
-  // KV-update prologue and land while the prologue runs.  (Issuing them
-  // after the prologue's own loads, unconditionally, measured slower in the
-  // model: duplicate chunks for idle waves and unclean chunks cost more port
-  // bytes than the in-order wait saves.)
+  // the request (host-computed `clean`): its loads go out right after the
+  // KV-update prologue's own loads (kv_update_item's after_loads hook) and
+  // land while the prologue computes and stores.  Only clean chunks of busy
+  // waves are prefetched: issuing every wave's first chunk unconditionally
+  // measured slower in the model (duplicate chunks for idle waves and unclean
+  // chunks cost more port bytes than the in-order wait saves).
   const int nchunks = (w.kv_len + 31) >> 5;
   h8 kf0[2][KS], va0[DT];
   const bool early = FUSED && wave < nchunks && (wave + 1) * 32 <= clean;
-  if (early) load_chunk(wave, kf0, va0);
 
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
   __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
@@ -401,7 +433,12 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     // (2) RoPE + KV store + staging of this item's tokens, this head
     kv_update_item<D, NQ, 64 * NW>(
         bv, &bv.work[blockIdx.x], h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
-        qbuf, kc, kv.stage_wr, sV, sSlot, sQ, [] {});
+        qbuf, kc, kv.stage_wr, sV, sSlot, sQ, [&] {
+          // the first clean chunk goes out once the prologue's own loads are
+          // in flight (issued earlier, every prologue wait -- the commit
+          // records, the token records -- also waited for these 24 loads)
+          if (early) load_chunk(wave, kf0, va0);
+        });
     stamp(7);
     __syncthreads();
     stamp(8);
