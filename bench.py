@@ -221,6 +221,10 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", rank))
     if world != args.gpus:
         raise SystemExit(f"WORLD_SIZE {world} != --gpus {args.gpus}")
+    if world > 1:
+        # single node: RCCL's bootstrap over loopback (the data path is
+        # xGMI peer-to-peer); an interface the user set wins
+        os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     port = int(os.environ.get("MASTER_PORT", 29500)) + 31
     ctrl = Ctrl(rank, world, port)
     fa.set_device(local)
