@@ -233,3 +233,22 @@ def test_single_request_and_queued_requests():
     for a, r in zip(solo, res[:3]):
         if a != r.output_tokens:
             assert first_divergence(a, r.output_tokens) > 0
+
+
+def test_weight_stream_policy_same_tokens(monkeypatch):
+    """FFMI_W_STREAM (non-temporal weight loads; on by default only for
+    models larger than the Infinity Cache, so the small test models run
+    without it) changes no token: forced on vs forced off, incr decoding
+    and SpecInfer."""
+    ps = prompts(4, 1000, 5, 40, 8)
+
+    def both():
+        inc, _ = run_incr(ps, 70)
+        spec, _ = run_spec(ps, 70, SSM_CFG, 5)
+        return [r.output_tokens for r in inc], [r.output_tokens for r in spec]
+
+    monkeypatch.setenv("FFMI_W_STREAM", "1")
+    on = both()
+    monkeypatch.setenv("FFMI_W_STREAM", "0")
+    off = both()
+    assert on == off
