@@ -366,8 +366,13 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
   if (ntiles >= 512 || MT >= 8)
     return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
   // ... and where each wave still gets a full batch of U k-steps (K = 768 of
-  // the SSM: 4 waves x 6 k-steps beat 8 x 3, qkv T = 24: 5.7 -> 4.2 us)
-  if ((KT + S - 1) / S >= 8 * U)
+  // the SSM: 4 waves x 6 k-steps beat 8 x 3, qkv T = 24: 5.7 -> 4.2 us).
+  // Non-temporal weight loads (FFMI_W_STREAM) keep 4 waves at every row-tile
+  // count (LLaMA-7B decode, cold, T = 1-16: o 7.6-8.8 -> 7.2-8.6 us, down
+  // 17.0-24.8 -> 16.4-21.9 us over two runs of gemm_bench.py --wstream; T = 32
+  // within noise), so a row's reduction order still depends on (N-tile, K,
+  // policy) only, not on T.
+  if ((KT + S - 1) / S >= 8 * U && !nt)
     return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
   return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
 }

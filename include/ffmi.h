@@ -166,8 +166,10 @@ typedef enum {
 #define FFMI_Y_PACKED 0x20
 /* OR into `epilogue`: the weights are a once-read stream (a model larger than
  * the 256 MiB Infinity Cache): their loads carry the non-temporal hint so they
- * do not evict the KV cache, activations or a small model's weights.  Speed
- * only; results are identical. */
+ * do not evict the KV cache, activations or a small model's weights.  Long-K
+ * launches of <= 64 rows then split K over 4 waves instead of 8 (faster under
+ * the hint): results within the GEMM tolerance of the default policy, and
+ * still independent of T within the <= 64-row regime. */
 #define FFMI_W_STREAM 0x40
 size_t ffmi_packed_activation_bytes(int T, int in_dim);
 ffmi_status ffmi_pack_activations(const void *X, int T, int in_dim, void *X_packed,

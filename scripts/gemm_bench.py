@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--T", default="1,8,24,64,168,192")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--xpacked", action="store_true", help="pre-pack X (FFMI_X_PACKED)")
+    ap.add_argument("--wstream", action="store_true",
+                    help="non-temporal weight loads (FFMI_W_STREAM, as the LLaMA-7B model)")
     ap.add_argument("--ops", default="", help="comma list of op names to run (default all)")
     ap.add_argument("--cold-mb", type=int, default=768,
                     help="rotate weight copies totalling this many MB (0: one hot copy)")
@@ -70,6 +72,8 @@ def main():
                     F.check(L.ffmi_pack_activations(xb.ptr, T, K, xp.ptr, None))
                     packed.append(xp)
                 Xs = packed
+            if args.wstream:
+                flag |= F.W_STREAM
             Y = Buf.empty((T, N), np.float16)
             for i in range(len(Wps)):
                 F.check(L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None))

@@ -171,9 +171,12 @@ def test_linear_gate_up_silu_fused(T):
 
 
 @pytest.mark.parametrize("Ts", [(1, 8, 40, 64), (65, 100, 168, 192)])
-def test_linear_rows_independent_of_batch(Ts):
-    # within a kernel regime (skinny: T <= 64, M-split: T > 64) a row's
-    # reduction order must not depend on T (batching invariance)
+@pytest.mark.parametrize("wstream", [0, 1])
+def test_linear_rows_independent_of_batch(Ts, wstream):
+    # within a kernel regime (skinny: T <= 64, M-split: T > 64) and weight
+    # policy, a row's reduction order must not depend on T (batching
+    # invariance)
+    flag = F.W_STREAM if wstream else 0
     rng = np.random.default_rng(1)
     N, K = 1024, 2048
     X = f16(rng.standard_normal((max(Ts), K)))
@@ -182,7 +185,7 @@ def test_linear_rows_independent_of_batch(Ts):
     outs = []
     for T in Ts:
         Xb, Yb = Buf(X[:T]), Buf.empty((T, N), np.float16)
-        F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Yb.ptr, T, N, K, F.EPI_NONE, None))
+        F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Yb.ptr, T, N, K, F.EPI_NONE | flag, None))
         outs.append(Yb.get())
     for o in outs[:-1]:
         assert np.array_equal(o.view(np.uint16), outs[-1][:o.shape[0]].view(np.uint16))
@@ -570,12 +573,15 @@ def test_allreduce_single_rank_and_silu():
 
 @pytest.mark.parametrize("T", [1, 8, 24, 64, 168, 300])
 @pytest.mark.parametrize("epi", [0, 1])
-def test_linear_weight_stream_hint_bit_identical(T, epi):
-    """FFMI_W_STREAM (non-temporal weight loads) changes the cache policy
-    only: skinny, M-split (one and several row blocks) and split-K paths give
-    the same bits as the default policy."""
+@pytest.mark.parametrize("K", [1024, 4096])
+def test_linear_weight_stream_hint(T, epi, K):
+    """FFMI_W_STREAM (non-temporal weight loads): M-split launches (one and
+    several row blocks) and short-K skinny launches give the same bits as the
+    default policy; long-K skinny launches (>= 8 batches of k-steps per wave
+    at 8 waves) keep 4 waves under the hint, a different fp32 summation
+    order, so there the two policies agree within the oracle tolerance."""
     rng = np.random.default_rng(2000 + T + epi)
-    N, K = 1024, 2048
+    N = 1024
     X = f16(rng.standard_normal((T, K)))
     if epi:
         Wg, Wu = f16(rng.uniform(-0.05, 0.05, (N, K))), f16(rng.uniform(-0.05, 0.05, (N, K)))
@@ -588,4 +594,8 @@ def test_linear_weight_stream_hint_bit_identical(T, epi):
     Y0, Y1 = Buf.empty((T, N), np.float16), Buf.empty((T, N), np.float16)
     F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y0.ptr, T, N, K, epi, None))
     F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Y1.ptr, T, N, K, epi | F.W_STREAM, None))
-    assert np.array_equal(Y0.get().view(np.uint16), Y1.get().view(np.uint16))
+    U = 8 if T <= 32 else 4  # k-steps per batch of the skinny kernel (dispatch_nt)
+    if T > 64 or epi or K // 32 < 8 * U:
+        assert np.array_equal(Y0.get().view(np.uint16), Y1.get().view(np.uint16))
+    else:
+        close16(Y1.get(), Y0.get().astype(np.float32), max_ulp=2, exact_frac=0.9)
