@@ -117,6 +117,22 @@ class Ctrl:
         self.max(0.0)
 
 
+def stdout_to_stderr(fn):
+    """Run fn with file descriptor 1 pointed at stderr: RCCL prints a version
+    banner on stdout at communicator creation, and stdout must carry only
+    rank 0's JSON line."""
+    import ctypes
+    sys.stdout.flush()
+    saved = os.dup(1)
+    os.dup2(2, 1)
+    try:
+        return fn()
+    finally:
+        ctypes.CDLL(None).fflush(None)
+        os.dup2(saved, 1)
+        os.close(saved)
+
+
 def device_sync():
     import ctypes
     h = ctypes.CDLL("libamdhip64.so.7")
@@ -230,8 +246,8 @@ def main():
     fa.set_device(local)
     comm = None
     if world > 1:
-        uid = ctrl.bcast(fa.Comm.unique_id() if rank == 0 else b"")
-        comm = fa.Comm(uid, world, rank)
+        uid = ctrl.bcast(stdout_to_stderr(fa.Comm.unique_id) if rank == 0 else b"")
+        comm = stdout_to_stderr(lambda: fa.Comm(uid, world, rank))
 
     llm_cfg = fa.llama_config_from_hf(args.llm_weights) if args.llm_weights else dict(LLAMA_7B)
     ssm_cfg = fa.llama_config_from_hf(args.ssm_weights) if args.ssm_weights else dict(LLAMA_68M)

@@ -17,7 +17,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import flexflow_amd as fa  # noqa: E402
-from bench import LLAMA_65B, LLAMA_68M, LLAMA_7B, make_prompts  # noqa: E402
+from bench import LLAMA_65B, LLAMA_68M, LLAMA_7B, make_prompts, stdout_to_stderr  # noqa: E402
 
 
 def main():
@@ -30,7 +30,7 @@ def main():
     cfg = LLAMA_65B if args.model == "65b" else LLAMA_7B
     spec = args.mode == "spec"
     fa.set_device(0)
-    comm = fa.Comm(fa.Comm.unique_id(), 1, 0)
+    comm = stdout_to_stderr(lambda: fa.Comm(stdout_to_stderr(fa.Comm.unique_id), 1, 0))
     B, P, D, tree, mtb = 8, 128, 128, 23, 1024
     rm_kw = dict(max_requests_per_batch=B, max_tokens_per_batch=mtb,
                  max_spec_tree_token_num=tree, max_sequence_length=512)
