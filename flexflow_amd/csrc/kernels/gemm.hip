@@ -674,7 +674,11 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       const double tstep = base[o] * (ntw + 4.0 * p.MTW) / (ntw + 12.0);
       double t = rounds * (steps * tstep + 4.0);
       const double slab_mb = (double)S * T * ntiles * 16 * 4 / 1e6;
-      if (S > 1) t += deferred ? slab_mb / 6.0 : 3.0 + slab_mb / 3.0;
+      // slabs cost their write here and their read in the consumer; a
+      // deferred read (norm / attention prologue) is no cheaper than the
+      // reduce pass's: /6 had picked 8 slabs for LLaMA-7B o_proj at T = 168,
+      // 4 tiles x 4 slabs ran 0.6 % faster end to end (3 of 3 A/B pairs)
+      if (S > 1) t += deferred ? slab_mb / 3.0 : 3.0 + slab_mb / 3.0;
       if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
     }
   }
