@@ -11,5 +11,5 @@ for P in "$@"; do
 import json
 for l in open('gpurun_out/eb.json'):
     if l.startswith('{'):
-        d=json.loads(l); print(d['value'], d['time_split_ms_per_generate'], d['incr_decoding']['value'])"
+        d=json.loads(l); o=d.get('op_breakdown_sampled', {}); print(d['value'], d['time_split_ms_per_generate'], d.get('incr_decoding', {}).get('value'), {k: v['avg_us'] for k, v in o.items()})"
 done

@@ -1,6 +1,9 @@
 #!/bin/bash
-# Bench A/B of library build variants: scripts/gpu_lib_ab.sh "" nt ...
-# ("" = libffmi.so, "nt" = libffmi_nt.so built with EXTRA=-DFFMI_NT_WEIGHTS=1).
+# Bench A/B of library build variants: scripts/gpu_lib_ab.sh "" v2 ...
+# ("" = libffmi.so; "v2" = flexflow_amd/libffmi_v2.so, built beforehand with
+#  make -C flexflow_amd/csrc BUILD=build_v2 OUT=../libffmi_v2.so EXTRA=-D...;
+#  the round-1 weight-cache-policy trial was run this way before it became
+#  the FFMI_W_STREAM flag).
 # Each variant runs SpecInfer (with the incr side run) twice, alternating.
 set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
