@@ -56,6 +56,7 @@ struct LlamaGPU : public ffmi_model {
   float *ws = nullptr;  // split-K workspace of the GEMMs
   size_t ws_bytes = 0;
   int32_t *ids_h = nullptr;
+  bool result_copy = getenv("FFMI_RESULT_COPY") && atoi(getenv("FFMI_RESULT_COPY")) != 0;
   float *probs_h = nullptr;
   ffmi_batch_dev *batch = nullptr;
   PackedStep ps;
@@ -518,14 +519,20 @@ struct LlamaGPU : public ffmi_model {
     TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
     pr = prof_begin(ptail);
-    // ids [T*k] then probs [T*k] back to back: one result copy per step
-    float *probs_d = reinterpret_cast<float *>(ids_d + (size_t)T * k);
+    // ids [T*k] then probs [T*k] back to back.  The sampling kernel writes
+    // them straight into the pinned host buffer (a few bytes per row over
+    // PCIe, visible after the stream synchronisation like a copy kernel's
+    // stores), so a step needs no result-copy launch; FFMI_RESULT_COPY=1
+    // keeps the device buffer + copy (A/B runs)
+    int32_t *ids_o = result_copy ? ids_d : ids_h;
+    float *probs_o = reinterpret_cast<float *>(ids_o + (size_t)T * k);
     if (k == 1)
-      TRY(ffmi_argmax(logits, T, V, ids_d, probs_d, s));
+      TRY(ffmi_argmax(logits, T, V, ids_o, probs_o, s));
     else
-      TRY(ffmi_arg_topk(logits, T, V, k, ids_d, probs_d, s));
+      TRY(ffmi_arg_topk(logits, T, V, k, ids_o, probs_o, s));
     prof_end(pr, SAMPLING, (double)T * V * 2, 0);
-    FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));
+    if (result_copy)
+      FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));
 #undef TRY
     return FFMI_OK;
   }
