@@ -63,7 +63,13 @@ def llama_config_from_hf(src: Union[str, Mapping]) -> dict:
     # llama3 RoPE scaling: the reference reads it under "scaling_factor",
     # HF configs under "rope_scaling" or "rope_parameters"
     sc = c.get("scaling_factor") or c.get("rope_scaling") or rp
-    if isinstance(sc, Mapping) and sc.get("rope_type", sc.get("type")) == "llama3":
+    kind = sc.get("rope_type", sc.get("type")) if isinstance(sc, Mapping) else None
+    if kind not in (None, "default", "llama3"):
+        # the reference applies only plain and llama3 RoPE (inc_multihead_self_attention.cu:
+        # 703-722); loading another scaling (linear, dynamic, yarn, ...) unscaled would
+        # decode wrongly without any error
+        raise ValueError(f"unsupported rope scaling type {kind!r} (supported: default, llama3)")
+    if kind == "llama3":
         cfg.update(rope_llama3=1, rope_factor=float(sc["factor"]),
                    rope_low_freq_factor=float(sc["low_freq_factor"]),
                    rope_high_freq_factor=float(sc["high_freq_factor"]),

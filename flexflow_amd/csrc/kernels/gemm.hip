@@ -371,8 +371,9 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
   // count (LLaMA-7B decode, cold, T = 1-16: o 7.6-8.8 -> 7.2-8.6 us, down
   // 17.0-24.8 -> 16.4-21.9 us over two runs of gemm_bench.py --wstream; T = 32
   // within noise), so a row's reduction order still depends on (N-tile, K,
-  // policy) only, not on T.
-  if ((KT + S - 1) / S >= 8 * U && !nt)
+  // policy) only, not on T: the threshold is a fixed 64 k-steps per slice
+  // (8 waves x the largest batch U = 8), never U itself, which depends on T.
+  if ((KT + S - 1) / S >= 64 && !nt)
     return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
   return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
 }

@@ -59,3 +59,17 @@ def test_hf_model_conversion_writes_the_reference_files(tmp_path):
         b = np.fromfile(tmp_path / "st" / name, np.uint16)
         assert np.array_equal(a, b), name
     assert fa.llama_config_from_hf(str(tmp_path / "hf")) == CFG
+
+
+@pytest.mark.parametrize("kind", ["linear", "dynamic", "yarn"])
+def test_unsupported_rope_scaling_is_rejected(kind):
+    """Only plain and llama3 RoPE exist in the reference
+    (inc_multihead_self_attention.cu:703-722): another scaling type must fail
+    loudly instead of loading unscaled."""
+    hf = dict(num_attention_heads=4, num_hidden_layers=1, vocab_size=64, hidden_size=64,
+              intermediate_size=128, rms_norm_eps=1e-6, rope_theta=10000.0,
+              rope_scaling={"rope_type": kind, "factor": 2.0})
+    with pytest.raises(ValueError, match="rope scaling"):
+        fa.llama_config_from_hf(hf)
+    hf["rope_scaling"] = {"rope_type": "default"}
+    assert "rope_llama3" not in fa.llama_config_from_hf(hf)
