@@ -110,13 +110,37 @@ static inline float dot8(const float *a, const float *b, int K) {
   return ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
 }
 
+// Reference fp16 compute type (fp16 == ORC_REF16): cublasGemmEx with
+// compute_type = output_type = half (linear_kernels.cu:493-528; the prompt
+// attention GEMMs likewise, inc_multihead_self_attention.cu:108-200).  The
+// accumulator is a half; modelled as tensor-core MMA steps of g_ref_block
+// products (fp16 x fp16 products are exact in fp32) summed in fp32 and added
+// to the half accumulator with one rounding per step.  cuBLAS's kernel choice
+// (k per MMA, split-K) is not pinned by anything the reference holds, so the
+// block is a parameter (orc_set_ref_block; default 16 = mma.m16n8k16).
+static int g_ref_block = 16;
+extern "C" void orc_set_ref_block(int k) { g_ref_block = k > 0 ? k : 16; }
+
+static inline float dot_ref16(const float *a, const float *b, int K) {
+  float acc = 0.f;
+  for (int k0 = 0; k0 < K; k0 += g_ref_block) {
+    const int k1 = std::min(K, k0 + g_ref_block);
+    float s = 0.f;
+    for (int k = k0; k < k1; ++k) s += a[k] * b[k];
+    acc = orc_round16(acc + s);
+  }
+  return acc;
+}
+
 // linear_kernels.cu:450-582 (cublasGemmEx OP_T/OP_N, out = in . W^T).
 extern "C" void orc_linear(const float *X, const float *W, float *Y, int T,
                            int N, int K, int fp16) {
 #pragma omp parallel for schedule(static)
   for (int n = 0; n < N; ++n) {
     const float *w = W + (size_t)n * K;
-    for (int t = 0; t < T; ++t) Y[(size_t)t * N + n] = R(dot8(X + (size_t)t * K, w, K), fp16);
+    for (int t = 0; t < T; ++t)
+      Y[(size_t)t * N + n] = fp16 == ORC_REF16 ? dot_ref16(X + (size_t)t * K, w, K)
+                                               : R(dot8(X + (size_t)t * K, w, K), fp16);
   }
 }
 
@@ -252,6 +276,40 @@ extern "C" void orc_attention_row(const float *q, const float *K,
     for (int i = 0; i < d; ++i) out[i] += w * v[i];
   }
   for (int i = 0; i < d; ++i) out[i] = R(out[i], fp16);
+}
+
+// Prompt-phase attention of IncMultiHeadSelfAttention / SpecInc
+// (compute_attention_kernel_prompt, inc_multihead_self_attention.cu:98-366)
+// for ONE head of one request: T_new queries at positions start..start+T_new-1
+// against keys 0..start+T_new-1.
+//   QK^T: cublasGemmStridedBatchedEx, half compute type, alpha = (DT)(1/sqrt d)
+//         (:154-157) -> scores = half(alpha16 * acc16);
+//   fill_entries_above_diagonal -> -inf (:222-236);
+//   cudnnSoftmaxForward, half in/out (:238-262);
+//   softmax . V: half compute type (:264-300), stored as half.
+// q [T_new][d], K/V [nk][d] (half-representable), out [T_new][d].
+extern "C" void orc_attention_prompt_ref16(const float *q, const float *K, const float *V,
+                                           int T_new, int start, int d, float *out) {
+  const int nk = start + T_new;
+  const float alpha = orc_round16(1.0f / sqrtf((float)d));
+  std::vector<float> sc(nk), pr(nk), vt((size_t)d * nk);
+  for (int j = 0; j < nk; ++j)
+    for (int i = 0; i < d; ++i) vt[(size_t)i * nk + j] = V[(size_t)j * d + i];
+  for (int t = 0; t < T_new; ++t) {
+    const int pos = start + t;
+    float mx = -INFINITY;
+    for (int j = 0; j <= pos; ++j) {
+      sc[j] = orc_round16(alpha * dot_ref16(q + (size_t)t * d, K + (size_t)j * d, d));
+      mx = std::max(mx, sc[j]);
+    }
+    double sum = 0.0;
+    for (int j = 0; j < nk; ++j) {
+      pr[j] = j <= pos ? expf(sc[j] - mx) : 0.f;
+      sum += pr[j];
+    }
+    for (int j = 0; j < nk; ++j) pr[j] = orc_round16(pr[j] / (float)sum);
+    for (int i = 0; i < d; ++i) out[(size_t)t * d + i] = dot_ref16(pr.data(), &vt[(size_t)i * nk], nk);
+  }
 }
 
 // softmax over the vocab (softmax.cu:262-288; output stored as T), then the
@@ -396,8 +454,19 @@ extern "C" long orc_model_weight(orc_model *m, const char *name, float *out) {
   return (long)src->size();
 }
 
+extern "C" int orc_model_forward_ex(orc_model *m, int req, const int *tokens, int T,
+                                    int start_pos, float *logits, int prompt_phase);
 extern "C" int orc_model_forward(orc_model *m, int req, const int *tokens, int T,
                                  int start_pos, float *logits) {
+  return orc_model_forward_ex(m, req, tokens, T, start_pos, logits, 0);
+}
+
+// prompt_phase != 0 with fp16 == ORC_REF16: the attention of these T tokens
+// takes the reference's prompt path (orc_attention_prompt_ref16) instead of
+// the generation kernel's fp32 softmax -- as IncMHA does for a request in its
+// prompt phase (inc_multihead_self_attention.cu:944-985).
+extern "C" int orc_model_forward_ex(orc_model *m, int req, const int *tokens, int T,
+                                    int start_pos, float *logits, int prompt_phase) {
   const orc_config &c = m->c;
   const int H = c.hidden, F = c.intermediate, d = m->d, nh = c.num_heads;
   const int fp16 = m->fp16;
@@ -450,6 +519,15 @@ extern "C" int orc_model_forward(orc_model *m, int req, const int *tokens, int T
         for (int j = 0; j < nk; ++j) {
           memcpy(&Kh[(size_t)j * d], kc + (size_t)j * H + hd * d, d * sizeof(float));
           memcpy(&Vh[(size_t)j * d], vc + (size_t)j * H + hd * d, d * sizeof(float));
+        }
+        if (prompt_phase && fp16 == ORC_REF16) {
+          std::vector<float> qh((size_t)T * d), oh((size_t)T * d);
+          for (int t = 0; t < T; ++t)
+            memcpy(&qh[(size_t)t * d], &q[(size_t)t * H + hd * d], d * sizeof(float));
+          orc_attention_prompt_ref16(qh.data(), Kh.data(), Vh.data(), T, start_pos, d, oh.data());
+          for (int t = 0; t < T; ++t)
+            memcpy(&att[(size_t)t * H + hd * d], &oh[(size_t)t * d], d * sizeof(float));
+          continue;
         }
         for (int t = 0; t < T; ++t) {
           int pos = start_pos + t;

@@ -37,6 +37,13 @@ typedef struct {
   float rope_theta;
 } orc_config;
 
+/* `fp16` argument values: 0 = full precision (--use-full-precision), 1 =
+ * half storage with fp32 accumulation (the MI355X path's semantics), 2 =
+ * ORC_REF16: half storage AND the reference's half compute type in the dense
+ * and prompt-attention GEMMs (linear_kernels.cu:493-528,
+ * inc_multihead_self_attention.cu:98-366). */
+#define ORC_REF16 2
+
 /* ---- fp16 helpers (RNE) ---- */
 uint16_t orc_f2h(float f);
 float orc_h2f(uint16_t h);
@@ -55,6 +62,14 @@ void orc_gen_weight(const char *name, uint64_t seed, int kind, size_t n,
  * accumulate -- the reference's fp16 compute type is a documented deviation) */
 void orc_linear(const float *X, const float *W, float *Y, int T, int N, int K,
                 int fp16);
+/* MMA block (products summed in fp32 per step) of the ORC_REF16 half
+ * accumulator model; default 16 */
+void orc_set_ref_block(int k);
+/* Prompt-phase attention of one head (inc_multihead_self_attention.cu:98-366)
+ * with the reference's half compute type: q [T_new][d] at positions
+ * start..start+T_new-1, K/V [start+T_new][d], out [T_new][d]. */
+void orc_attention_prompt_ref16(const float *q, const float *K, const float *V, int T_new,
+                                int start, int d, float *out);
 /* RMSNorm (rms_norm_kernels.cu:97-124) */
 void orc_rmsnorm(const float *X, const float *w, float *out, int T, int H,
                  float eps, int fp16);
@@ -98,6 +113,11 @@ void orc_model_reset(orc_model *m, int req);
  * (causal, KV cache kept per request).  logits: [T][V] or NULL. */
 int orc_model_forward(orc_model *m, int req, const int *tokens, int T,
                       int start_pos, float *logits);
+/* as orc_model_forward; prompt_phase != 0 in ORC_REF16 mode runs the
+ * attention through the reference's prompt path (cuBLAS/cuDNN half
+ * semantics) instead of the generation kernel's */
+int orc_model_forward_ex(orc_model *m, int req, const int *tokens, int T,
+                         int start_pos, float *logits, int prompt_phase);
 /* Batched decode step for the CPU baseline: token t belongs to request
  * reqs[t] at position pos[t] (one token per request, caches as above); the
  * dense layers read every weight once for the whole batch. */

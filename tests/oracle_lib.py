@@ -64,6 +64,11 @@ def lib():
         L.orc_model_destroy.argtypes = [ctypes.c_void_p]
         L.orc_model_forward.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
                                         ctypes.c_int, ctypes.c_int, _f32p]
+        L.orc_model_forward_ex.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p, ctypes.c_int,
+                                           ctypes.c_int, _f32p, ctypes.c_int]
+        L.orc_set_ref_block.argtypes = [ctypes.c_int]
+        L.orc_attention_prompt_ref16.argtypes = [_f32p, _f32p, _f32p] + [ctypes.c_int] * 3 + [
+            _f32p]
         L.orc_model_decode_batch.argtypes = [ctypes.c_void_p, _i32p, _i32p, _i32p,
                                              ctypes.c_int, _f32p]
         L.orc_model_get_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
@@ -82,6 +87,23 @@ def fp(a):
 
 def ip(a):
     return a.ctypes.data_as(_i32p)
+
+
+REF16 = 2  # oracle.h ORC_REF16: the reference's half compute type in GEMMs / prompt attention
+
+
+def set_ref_block(k):
+    lib().orc_set_ref_block(k)
+
+
+def attention_prompt_ref16(q, K, V, start):
+    q = np.ascontiguousarray(q, np.float32)
+    K = np.ascontiguousarray(K, np.float32)
+    V = np.ascontiguousarray(V, np.float32)
+    T, d = q.shape
+    out = np.empty((T, d), np.float32)
+    lib().orc_attention_prompt_ref16(fp(q), fp(K), fp(V), T, start, d, fp(out))
+    return out
 
 
 def round16(x):
@@ -197,6 +219,26 @@ class Model:
         rc = lib().orc_model_forward(self.h, req, ip(tokens), T, start_pos, fp(logits))
         assert rc == 0
         return logits
+
+    def forward_ex(self, req, tokens, start_pos, prompt_phase):
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        T = tokens.shape[0]
+        logits = np.empty((T, self.cfg["vocab_size"]), np.float32)
+        rc = lib().orc_model_forward_ex(self.h, req, ip(tokens), T, start_pos, fp(logits),
+                                        int(prompt_phase))
+        assert rc == 0
+        return logits
+
+    def teacher_forced_ref(self, seq, n_prompt, req=0):
+        """Logits the reference would compute along `seq`: the prompt
+        (seq[:n_prompt]) in one prompt-phase step, then every later token in
+        its own decode step (generation kernel), as incr_decoding runs it
+        (request_manager.cc:713-1135).  Returns the logits rows that pick
+        seq[n_prompt:] ([len(seq) - n_prompt][V])."""
+        rows = [self.forward_ex(req, seq[:n_prompt], 0, 1)[-1]]
+        for i in range(n_prompt, len(seq) - 1):
+            rows.append(self.forward_ex(req, seq[i:i + 1], i, 0)[0])
+        return np.stack(rows)
 
     def decode_batch(self, reqs, tokens, pos):
         reqs = np.ascontiguousarray(reqs, np.int32)

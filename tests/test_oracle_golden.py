@@ -77,3 +77,67 @@ def test_oracle_batched_decode_matches_per_request():
     for r in range(3):
         ls = m2.forward(r, [nxt[r]], pos[r])
         np.testing.assert_array_equal(lb[r], ls[0])
+
+
+# ------------------------------------------------- reference half compute type
+def _np_dot_ref16(a, b, block):
+    """numpy twin of the ORC_REF16 accumulator: per MMA step of `block`
+    products, an fp32 sum added to a half accumulator with one rounding."""
+    acc = np.float16(0)
+    for k0 in range(0, len(a), block):
+        s = np.float32(0)
+        for x, y in zip(a[k0:k0 + block], b[k0:k0 + block]):
+            s = np.float32(s + np.float32(x) * np.float32(y))
+        acc = np.float16(np.float32(acc) + s)
+    return np.float32(acc)
+
+
+@pytest.mark.parametrize("block", [16, 32])
+def test_ref16_linear_matches_numpy_twin(block):
+    rng = np.random.default_rng(block)
+    X = O.round16(rng.standard_normal((3, 200)))
+    W = O.round16(rng.uniform(-0.1, 0.1, (5, 200)))
+    O.set_ref_block(block)
+    try:
+        Y = O.linear(X, W, fp16=O.REF16)
+    finally:
+        O.set_ref_block(16)
+    ref = np.array([[_np_dot_ref16(x, w, block) for w in W] for x in X], np.float32)
+    assert np.array_equal(Y, ref)
+    # the half accumulator is measurably coarser than fp32 accumulation
+    assert not np.array_equal(Y, O.linear(X, W, fp16=1))
+
+
+def test_ref16_prompt_attention_matches_numpy_twin():
+    """inc_multihead_self_attention.cu:98-366: half(alpha16 * acc16(q.k)),
+    causal -inf fill, half softmax, half-accumulated P.V."""
+    rng = np.random.default_rng(7)
+    d, start, T = 64, 3, 5
+    nk = start + T
+    q = O.round16(rng.standard_normal((T, d)))
+    K = O.round16(rng.standard_normal((nk, d)))
+    V = O.round16(rng.standard_normal((nk, d)))
+    out = O.attention_prompt_ref16(q, K, V, start)
+    alpha = np.float32(np.float16(1.0 / np.sqrt(np.float32(d))))
+    for t in range(T):
+        pos = start + t
+        sc = np.array([np.float16(alpha * _np_dot_ref16(q[t], K[j], 16)) for j in range(pos + 1)],
+                      np.float32)
+        p = np.exp(sc - sc.max(), dtype=np.float32)
+        p = np.concatenate([p / np.float32(p.astype(np.float64).sum()), np.zeros(nk - pos - 1,
+                                                                                  np.float32)])
+        p = O.round16(p)
+        ref = np.array([_np_dot_ref16(p, V[:, i], 16) for i in range(d)], np.float32)
+        np.testing.assert_array_equal(out[t], ref)
+
+
+@pytest.mark.parametrize("tag", TAGS)
+def test_oracle_ref16_within_half_tolerance(tag):
+    # the reference's own semantics (half compute type, prompt path) against
+    # HF fp32 under its half-precision alignment bar
+    cfg, g = O.load_golden(tag)
+    m = O.Model(cfg, cfg["seed"], fp16=O.REF16)
+    logits = m.forward_ex(0, g["prompt"], 0, 1)
+    bad = np.abs(logits - g["logits"]) > 1e-2
+    assert bad.mean() <= 0.05
+    assert not np.array_equal(logits, O.Model(cfg, cfg["seed"], fp16=1).forward(0, g["prompt"], 0))
