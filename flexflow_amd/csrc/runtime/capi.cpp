@@ -24,6 +24,17 @@ extern "C" int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap) {
   return m->op_stats(out, cap);
 }
 
+extern "C" ffmi_status ffmi_model_set_debug(ffmi_model *m, int enable) {
+  if (!m) return FFMI_ERR_INVALID;
+  return m->set_debug(enable);
+}
+
+extern "C" long ffmi_model_debug_tensor(ffmi_model *m, int which, int layer, float *out,
+                                        long cap) {
+  if (!m || !out || cap <= 0) return -1;
+  return m->debug_tensor(which, layer, out, cap);
+}
+
 extern "C" ffmi_status ffmi_set_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FFMI_ERR_NO_DEVICE;

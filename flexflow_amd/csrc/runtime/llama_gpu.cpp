@@ -166,6 +166,50 @@ struct LlamaGPU : public ffmi_model {
     return b + (double)ps.tokens.size() * (3 * Hl + Hl) * 2;
   }
 
+  // ---- tensor capture (--inference-debugging, operator.h:271-360) ----
+  int dbg = 0;
+  uint16_t *dbg_buf = nullptr;  // [num_layers + 1][Tm][H] fp16 (last slot maybe packed)
+  int dbg_T = -1;
+  bool dbg_final_packed = false;
+  ffmi_status set_debug(int enable) override {
+    if (enable && !dbg_buf) {
+      const size_t Tm = (size_t)((o.max_tokens + 15) & ~15);
+      if (alloc(&dbg_buf, (size_t)(c.num_layers + 1) * Tm * c.hidden) != FFMI_OK)
+        return FFMI_ERR_OOM;
+    }
+    dbg = enable ? 1 : 0;
+    dbg_T = -1;
+    return FFMI_OK;
+  }
+  uint16_t *dbg_slot(int l) const {
+    const size_t Tm = (size_t)((o.max_tokens + 15) & ~15);
+    return dbg_buf + (size_t)l * Tm * c.hidden;
+  }
+  long debug_tensor(int which, int layer, float *out, long cap) override {
+    if (dbg_T < 0 || (stream && hipStreamSynchronize(stream) != hipSuccess)) return -1;
+    const int T = dbg_T, H = c.hidden, V = c.vocab_size;
+    const int width = which == FFMI_DBG_LOGITS ? V : H;
+    if ((which != FFMI_DBG_LOGITS && which != FFMI_DBG_HIDDEN) ||
+        (which == FFMI_DBG_HIDDEN && (layer < 0 || layer > c.num_layers)) ||
+        cap < (long)T * width)
+      return -1;
+    std::vector<uint16_t> h16((size_t)T * width);
+    const uint16_t *src = which == FFMI_DBG_LOGITS ? logits : dbg_slot(layer);
+    const bool pk = which == FFMI_DBG_HIDDEN && layer == c.num_layers && dbg_final_packed;
+    // a packed slot covers whole 16-row tiles
+    const size_t n = pk ? (size_t)((T + 15) & ~15) * width : (size_t)T * width;
+    std::vector<uint16_t> raw(n);
+    if (hipMemcpy(raw.data(), src, n * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
+    for (int t = 0; t < T; ++t)
+      for (int j = 0; j < width; ++j) {
+        const uint16_t b = raw[pk ? act_packed_off(t, j, width) : (size_t)t * width + j];
+        _Float16 v;
+        memcpy(&v, &b, 2);
+        out[(size_t)t * width + j] = (float)v;
+      }
+    return T;
+  }
+
   ~LlamaGPU() override {
     if (stream) (void)hipStreamSynchronize(stream);
     clear_graphs();
@@ -409,7 +453,7 @@ struct LlamaGPU : public ffmi_model {
     // graphed: small steps, and tree-verify steps of one work item per
     // request (a fixed shape while the batch is full: T = 168 for 8 requests
     // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
-    const bool graph = use_graphs && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
+    const bool graph = use_graphs && !dbg && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
                        o.tp_size == 1 && !prof_on(0, T) && !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
@@ -477,6 +521,9 @@ struct LlamaGPU : public ffmi_model {
                                     l == 0 ? ffmi::Partials() : down_part,
                                     l == 0 ? batch->dev : nullptr));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
+      if (dbg && l > 0)  // residual stream after layer l-1
+        FFMI_HIP(hipMemcpyAsync(dbg_slot(l - 1), res, (size_t)T * H * 2, hipMemcpyDeviceToDevice,
+                                stream));
       pr = prof_begin(on);
       ffmi::Partials qkv_part;
       FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
@@ -515,6 +562,15 @@ struct LlamaGPU : public ffmi_model {
     FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
                                   down_part));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+    if (dbg) {
+      FFMI_HIP(hipMemcpyAsync(dbg_slot(c.num_layers - 1), res, (size_t)T * H * 2,
+                              hipMemcpyDeviceToDevice, stream));
+      FFMI_HIP(hipMemcpyAsync(dbg_slot(c.num_layers), h,
+                              (size_t)(packed ? (T + 15) & ~15 : T) * H * 2,
+                              hipMemcpyDeviceToDevice, stream));
+      dbg_final_packed = packed;
+      dbg_T = T;
+    }
     pr = prof_begin(ptail);
     TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);

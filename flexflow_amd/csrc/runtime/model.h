@@ -57,6 +57,17 @@ struct ffmi_model {
     (void)cap;
     return 0;
   }
+  virtual ffmi_status set_debug(int enable) {
+    (void)enable;
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  virtual long debug_tensor(int which, int layer, float *out, long cap) {
+    (void)which;
+    (void)layer;
+    (void)out;
+    (void)cap;
+    return -1;
+  }
 };
 
 namespace ffmi {

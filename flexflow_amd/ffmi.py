@@ -21,6 +21,7 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "hip error", 3: "rccl error", 4: "o
           5: "unsupported", 6: "no gfx950 device"}
 ATTN_INC, ATTN_SPEC, ATTN_TREE = 0, 1, 2
 MODEL_INC, MODEL_BEAM, MODEL_TREE = 0, 1, 2
+DBG_HIDDEN, DBG_LOGITS = 0, 1  # ffmi_model_debug_tensor kinds
 EPI_NONE, EPI_SILU_MUL = 0, 1
 X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
 Y_PACKED = 0x20  # FFMI_Y_PACKED
@@ -147,6 +148,8 @@ SIGNATURES = {
     "ffmi_model_destroy": (None, [c_void_p]),
     "ffmi_model_set_profiling": (c_int, [c_void_p, c_int]),
     "ffmi_model_op_stats": (c_int, [c_void_p, ctypes.POINTER(OpStat), c_int]),
+    "ffmi_model_set_debug": (c_int, [c_void_p, c_int]),
+    "ffmi_model_debug_tensor": (ctypes.c_long, [c_void_p, c_int, c_int, c_void_p, ctypes.c_long]),
     "ffmi_set_device": (c_int, [c_int]),
     "ffmi_rm_create": (c_int, [ctypes.POINTER(RMConfig), ctypes.POINTER(c_void_p)]),
     "ffmi_rm_destroy": (None, [c_void_p]),

@@ -43,6 +43,24 @@ class Model:
         return {a.name.decode(): dict(launches=a.launches, ms=a.total_ms, bytes=a.bytes,
                                       flops=a.flops) for a in arr[:n]}
 
+    def set_debug(self, enable: bool = True):
+        """Keep the last step's per-layer hidden states and logits
+        (--inference-debugging, operator.h:271-360); steps run eager."""
+        F.check(F.lib().ffmi_model_set_debug(self.handle, int(enable)), "set_debug")
+
+    def debug_tensor(self, which: str, layer: int = 0):
+        """'hidden' (layer l < num_layers: residual stream after layer l;
+        layer == num_layers: final norm output) or 'logits', as fp32 [T][width]."""
+        import numpy as np
+        width = self.config["vocab_size"] if which == "logits" else self.config["hidden"]
+        kind = F.DBG_LOGITS if which == "logits" else F.DBG_HIDDEN
+        buf = np.empty(1024 * width, np.float32)
+        T = F.lib().ffmi_model_debug_tensor(self.handle, kind, layer,
+                                            buf.ctypes.data_as(ctypes.c_void_p), buf.size)
+        if T < 0:
+            raise F.FFMIError(f"debug_tensor({which}, {layer}): nothing captured")
+        return buf[:T * width].reshape(T, width).copy()
+
     def close(self):
         if getattr(self, "handle", None):
             F.lib().ffmi_model_destroy(self.handle)

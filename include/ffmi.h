@@ -300,6 +300,21 @@ typedef struct {
 } ffmi_op_stat;
 ffmi_status ffmi_model_set_profiling(ffmi_model *m, int level);
 int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap);
+/* Tensor capture for alignment checks (the reference's --inference-debugging
+ * per-layer dumps, operator.h:271-360, compared by
+ * tests/inference/inference_alignment_test.py).  While enabled, steps run
+ * eager (no graph replay) and the LAST step's tensors are kept on the device:
+ *   FFMI_DBG_HIDDEN, layer l in [0, num_layers): the residual stream after
+ *     decoder layer l (HF hidden_states[l + 1]); layer == num_layers: the
+ *     final RMSNorm output (HF's last hidden state);
+ *   FFMI_DBG_LOGITS: the lm_head output [T][vocab] (before softmax).
+ * ffmi_model_debug_tensor copies one as fp32 rows [T][width] into `out`
+ * (capacity `cap` floats) and returns T, or -1 (nothing captured / bad
+ * argument / too small).  Replicated under TP: every rank returns the same. */
+#define FFMI_DBG_HIDDEN 0
+#define FFMI_DBG_LOGITS 1
+ffmi_status ffmi_model_set_debug(ffmi_model *m, int enable);
+long ffmi_model_debug_tensor(ffmi_model *m, int which, int layer, float *out, long cap);
 /* select the HIP device of the calling thread (one process per GPU) */
 ffmi_status ffmi_set_device(int device);
 

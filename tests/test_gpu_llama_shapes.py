@@ -1,0 +1,85 @@
+"""Dense layers at the exact shapes the BASELINE configs run, with the flags
+the model uses (packed activation tiles in, W_STREAM non-temporal weight
+loads, the gate/up SiLU epilogue writing packed tiles out), against the CPU
+oracle's fp32-accumulate restatement (linear_kernels.cu:450-582).
+
+Shapes (SURVEY.md §8 constants):
+- LLaMA-7B, TP = 1 (configs B/C): qkv 12288x4096, o 4096x4096,
+  gate|up 2x11008x4096, down 4096x11008, lm_head 32000x4096;
+- LLaMA-65B, TP = 8 per-rank shards (configs D/E): qkv 3072x8192,
+  o 8192x1024, gate|up 2x2752x8192, down 8192x2752, lm_head vocab shard
+  4000x8192;
+- T = 8 (decode batch, skinny kernel) and T = 168 (8 requests x 21-token
+  verify trees, M-split kernel).
+Tolerance as test_gpu_kernels.close16: <= 2 fp16 ulp (or 1e-4 * max |ref|)
+everywhere and >= 99% of elements bit-identical (only the fp32 summation
+order differs).
+"""
+import zlib
+
+import numpy as np
+import pytest
+
+import flexflow_amd.ffmi as F
+import oracle_lib as O
+from hip_util import Buf, f16
+from test_gpu_kernels import close16, pack_act_np, unpack_act_np
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = {
+    "7b_qkv": (12288, 4096, 0), "7b_o": (4096, 4096, 0), "7b_gate_up": (11008, 4096, 1),
+    "7b_down": (4096, 11008, 0), "7b_lm_head": (32000, 4096, 0),
+    "65b_tp8_qkv": (3072, 8192, 0), "65b_tp8_o": (8192, 1024, 0),
+    "65b_tp8_gate_up": (2752, 8192, 1), "65b_tp8_down": (8192, 2752, 0),
+    "65b_tp8_lm_head_shard": (4000, 8192, 0),
+}
+
+
+@pytest.mark.parametrize("T", [8, 168])
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_linear_at_baseline_shapes(shape, T):
+    N, K, epi = SHAPES[shape]
+    L = F.lib()
+    rng = np.random.default_rng(zlib.crc32(f"{shape}:{T}".encode()))
+    X = f16(rng.standard_normal((T, K)))
+    amp = 0.02 * np.sqrt(3.0)  # the synthetic weights' range (orc_gen_weight kind 0)
+    if epi:
+        Wg, Wu = f16(rng.uniform(-amp, amp, (N, K))), f16(rng.uniform(-amp, amp, (N, K)))
+        gb, ub = Buf(Wg), Buf(Wu)
+        Wp = Buf.empty((2 * L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+        del gb, ub
+    else:
+        W = f16(rng.uniform(-amp, amp, (N, K)))
+        src = Buf(W)
+        Wp = Buf.empty((L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+        F.check(L.ffmi_linear_pack_weight(src.ptr, N, K, Wp.ptr, None))
+        del src
+    Xp = Buf(pack_act_np(X))
+    flags = epi | F.X_PACKED | F.W_STREAM | (F.Y_PACKED if epi else 0)
+    Tp = (T + 15) // 16 * 16
+    Y = Buf.empty(((Tp if epi else T), N), np.float16)
+    F.check(L.ffmi_linear(Xp.ptr, Wp.ptr, Y.ptr, T, N, K, flags, None), shape)
+    y = Y.get()
+    if epi:
+        y = unpack_act_np(y.reshape(-1), T, N)
+        g = O.linear(X.astype(np.float32), Wg.astype(np.float32))
+        u = O.linear(X.astype(np.float32), Wu.astype(np.float32))
+        ref = O.silu_mul(g, u)
+        # a 1-ulp flip of the rounded gate or up value (fp32 reordering at
+        # a rounding boundary) moves the output by ulp(g)*|u*dsilu| or
+        # ulp(u)*|silu(g)|, which can be many output ulps near zero: allow
+        # exactly that, per element
+        sg = 1.0 / (1.0 + np.exp(-g))
+        dsilu = sg * (1.0 + g * (1.0 - sg))
+        ulp = lambda x: np.spacing(np.abs(x).astype(np.float16)).astype(np.float32)  # noqa: E731
+        flip = 1.5 * (ulp(g) * np.abs(u * dsilu) + ulp(u) * np.abs(g * sg))
+        d = np.abs(y.astype(np.float32) - ref)
+        # (+ up to 3 ulp of the output from the chain's own roundings)
+        excess = d - (flip + 3 * ulp(ref))
+        assert (excess <= 0).all(), float(excess.max())
+        assert (y.astype(np.float16) == ref.astype(np.float16)).mean() >= 0.99
+    else:
+        ref = O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1)
+        close16(y, ref)
