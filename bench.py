@@ -20,13 +20,15 @@ import os
 import socket
 import statistics
 import struct
+import subprocess
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import flexflow_amd as fa  # noqa: E402  (load libffmi before anything else)
+fa = None  # flexflow_amd, imported by the rank processes only (after the launcher)
+CTRL_TIMEOUT_S = 600  # a control-plane peer silent this long is dead: fail, never hang
 
 LLAMA_7B = dict(num_layers=32, vocab_size=32000, num_heads=32, num_kv_heads=32, hidden=4096,
                 intermediate=11008, rms_eps=1e-6, rope_theta=10000.0)
@@ -56,7 +58,7 @@ def make_prompts(n, length, vocab, seed=20250117):
 class Ctrl:
     """Rank-0-hub TCP control plane (bytes broadcast, barrier, max)."""
 
-    def __init__(self, rank, world, port):
+    def __init__(self, rank, world, port, timeout=CTRL_TIMEOUT_S):
         self.rank, self.world = rank, world
         self.peers = []
         if world == 1:
@@ -66,20 +68,23 @@ class Ctrl:
             srv.setsockopt(socket.SOL_SOCKET, socket.SO_REUSEADDR, 1)
             srv.bind(("127.0.0.1", port))
             srv.listen(world)
+            srv.settimeout(timeout)  # a peer that never connects -> socket.timeout
             for _ in range(world - 1):
                 c, _ = srv.accept()
+                c.settimeout(timeout)
                 self.peers.append(c)
             srv.close()
         else:
-            deadline = time.time() + 300
+            deadline = time.time() + timeout
             while True:
                 try:
-                    self.sock = socket.create_connection(("127.0.0.1", port), timeout=300)
+                    self.sock = socket.create_connection(("127.0.0.1", port), timeout=timeout)
                     break
                 except OSError:
                     if time.time() > deadline:
                         raise
                     time.sleep(0.2)
+            self.sock.settimeout(timeout)
 
     @staticmethod
     def _recv(s, n):
@@ -146,21 +151,23 @@ def run_generate(rm, llm, prompts, max_length, spec):
     return new, lat, res
 
 
-def cpu_baseline(prompt_len=4, max_steps=96, budget_s=15.0, batch=8):
+def cpu_baseline(prompt_len=128, max_steps=128, budget_s=15.0, batch=8):
     """The CPU restatement (oracle/, test infrastructure) timed on the host:
     LLaMA-7B fp16-semantics incremental decoding, batch 8, batched decode
-    steps after a short prompt until ~budget_s of CPU work (a bounded sample
-    of the workload)."""
+    steps at the GPU run's decode positions (prompt_len, prompt_len + 1, ...)
+    until ~budget_s of CPU work (a bounded sample of the workload).  The
+    128-token prefill itself is not run -- at ~7 TMAC it alone would take
+    minutes on the host -- so the first prompt_len KV-cache rows hold zeros:
+    a timing sample (the attention reads the same number of keys as the GPU
+    run's decode steps), not a token-exact replay."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
 
     import oracle_lib as O
     m = O.Model(LLAMA_7B, 20250117, fp16=1, max_requests=batch,
                 max_seq=prompt_len + max_steps + 2)
-    prompts = make_prompts(batch, prompt_len, LLAMA_7B["vocab_size"], seed=7)
+    prompts = make_prompts(batch, 1, LLAMA_7B["vocab_size"], seed=7)
     reqs = np.arange(batch, dtype=np.int32)
-    for p in range(prompt_len):  # untimed prefill, one batched step per position
-        m.decode_batch(reqs, [pr[p] for pr in prompts], [p] * batch)
     toks = [pr[-1] for pr in prompts]
     t0 = time.time()
     steps = 0
@@ -171,8 +178,9 @@ def cpu_baseline(prompt_len=4, max_steps=96, budget_s=15.0, batch=8):
     dt = time.time() - t0
     return dict(value=round(batch * steps / dt, 3), unit="decoded tokens/s",
                 cores=int(O.lib().orc_num_threads()), kind="port",
-                sample=f"oracle LLaMA-7B incr decoding, batch {batch}, {steps} decode steps "
-                       f"after a {prompt_len}-token prompt, {dt:.1f}s")
+                sample=f"oracle LLaMA-7B incr decoding, batch {batch}, {steps} decode steps at "
+                       f"positions {prompt_len}-{prompt_len + steps - 1} (the GPU run's decode "
+                       f"range; prefill rows zero-filled, not computed), {dt:.1f}s")
 
 
 def pmc_traffic(kernel):
@@ -211,6 +219,44 @@ def pmc_mfma(hip_kernel):
     return None
 
 
+def launch_ranks(argv, n):
+    """`python bench.py --gpus N` with no RANK in the environment: start N
+    rank processes of this script (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    set, one GPU each) and exit with the worst status.  The launcher never
+    touches the GPU itself (no HIP call, no exec): it only spawns, waits and
+    kills.  Rank 0's stdout is ours (the JSON line); the others' go to
+    stderr."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(os.environ.get("MASTER_PORT", port)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                                      stdout=None if r == 0 else sys.stderr.fileno()))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                code = p.poll()
+                if code is None:
+                    continue
+                pending.remove(p)
+                if code != 0:
+                    rc = rc or code
+                    for q in pending:  # one rank died: the others would wait forever
+                        q.kill()
+            time.sleep(0.2)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+            p.wait()
+    return rc if rc > 0 else (1 if rc else 0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -230,8 +276,13 @@ def main():
                          "seeded synthetic LLaMA-7B)")
     ap.add_argument("--ssm-weights", default=None,
                     help="reference-format checkpoint folder of the SSM (default: synthetic 68M)")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launcher + control plane only, no GPU (CPU test of the N-rank path)")
+    ap.add_argument("--dry-run-fail-rank", type=int, default=-1, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
+    if args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(launch_ranks(sys.argv[1:], args.gpus))
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", args.gpus))
     local = int(os.environ.get("LOCAL_RANK", rank))
@@ -242,7 +293,19 @@ def main():
         # xGMI peer-to-peer); an interface the user set wins
         os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
     port = int(os.environ.get("MASTER_PORT", 29500)) + 31
+    if args.dry_run and rank == args.dry_run_fail_rank:
+        sys.exit(3)  # (test hook: a rank that dies before the control plane)
     ctrl = Ctrl(rank, world, port)
+    if args.dry_run:
+        ctrl.barrier()
+        t = ctrl.max(float(rank))
+        if rank == 0:
+            print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": world,
+                              "max_over_ranks": t}), flush=True)
+        return
+    global fa
+    import flexflow_amd  # loads libffmi (first HIP use is below)
+    fa = flexflow_amd
     fa.set_device(local)
     comm = None
     if world > 1:
@@ -340,8 +403,24 @@ def main():
             "host_scheduling": round((wall_us - llm_us - ssm_us) / 1e3 / args.steps, 1)},
     }
     if spec:
-        # tokens each request commits per verify step (incl. the bonus token)
-        out["tokens_per_request_verify"] = round(committed / max(1, req_verifies), 3)
+        # tokens each request commits per verify step (incl. the bonus token).
+        # With random weights the SSM's guesses match at chance level, so this
+        # is ~1.0: SpecInfer then pays a full verify step per token.  The
+        # acceptance-independent step costs are reported beside it, and the
+        # rate they imply at other acceptance levels is labelled a projection.
+        acc = committed / max(1, req_verifies)
+        out["acceptance"] = {"tokens_per_request_verify": round(acc, 3),
+                             "note": "random weights: SSM agreement at chance level"}
+        out["tokens_per_request_verify"] = round(acc, 3)
+        verify_ms = llm_us / 1e3 / max(1, llm_steps)
+        ssm_us_step = ssm_us / max(1, ssm_steps)
+        out["verify_step_ms"] = round(verify_ms, 3)
+        out["ssm_step_us"] = round(ssm_us_step, 1)
+        cycle_ms = verify_ms + ssm_us_step / 1e3 * (ssm_steps / max(1, llm_steps))
+        out["projection_tokens_per_s_at_acceptance"] = {
+            str(a): round(B * a / (cycle_ms / 1e3), 1) for a in (1, 2, 3, 4)}
+        out["projection_note"] = ("decode-phase rate B*a/(verify step + its SSM steps) from the "
+                                  "measured step costs; not a measurement")
     # roofline of the dominant kernel: the weight-streaming GEMM with the
     # largest sampled time (HIP events on the model stream, timed region)
     gemms = {k: v for k, v in ops.items() if k.startswith("gemm") and v["ms"] > 0}
