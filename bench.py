@@ -69,11 +69,13 @@ class Ctrl:
             srv.bind(("127.0.0.1", port))
             srv.listen(world)
             srv.settimeout(timeout)  # a peer that never connects -> socket.timeout
+            byrank = {}
             for _ in range(world - 1):
                 c, _ = srv.accept()
                 c.settimeout(timeout)
-                self.peers.append(c)
+                byrank[struct.unpack("<I", self._recv(c, 4))[0]] = c
             srv.close()
+            self.peers = [byrank[r] for r in sorted(byrank)]  # rank order
         else:
             deadline = time.time() + timeout
             while True:
@@ -85,6 +87,7 @@ class Ctrl:
                         raise
                     time.sleep(0.2)
             self.sock.settimeout(timeout)
+            self.sock.sendall(struct.pack("<I", rank))
 
     @staticmethod
     def _recv(s, n):
@@ -120,6 +123,27 @@ class Ctrl:
 
     def barrier(self):
         self.max(0.0)
+
+    def allgather(self, data: bytes):
+        """Every rank's bytes, in rank order, on every rank."""
+        if self.world == 1:
+            return [data]
+        if self.rank == 0:
+            parts = [data]
+            for p in self.peers:
+                n = struct.unpack("<I", self._recv(p, 4))[0]
+                parts.append(self._recv(p, n))
+            blob = b"".join(struct.pack("<I", len(x)) + x for x in parts)
+            self.bcast(blob)
+        else:
+            self.sock.sendall(struct.pack("<I", len(data)) + data)
+            blob = self.bcast(b"")
+        out, off = [], 0
+        while off < len(blob):
+            n = struct.unpack("<I", blob[off:off + 4])[0]
+            out.append(blob[off + 4:off + 4 + n])
+            off += 4 + n
+        return out
 
 
 def stdout_to_stderr(fn):
@@ -299,18 +323,53 @@ def main():
     if args.dry_run:
         ctrl.barrier()
         t = ctrl.max(float(rank))
+        g = ctrl.allgather(b"r%d" % rank)
         if rank == 0:
             print(json.dumps({"metric": "dry-run", "value": None, "n_gpus": world,
-                              "max_over_ranks": t}), flush=True)
+                              "max_over_ranks": t, "allgather": [x.decode() for x in g]}),
+                  flush=True)
         return
     global fa
     import flexflow_amd  # loads libffmi (first HIP use is below)
     fa = flexflow_amd
-    fa.set_device(local)
+    # FFMI_BENCH_DEVICE pins every rank to one device: a rehearsal of the
+    # N-rank path on a one-GPU box (with FFMI_TP_TRANSPORT=xgmi-only, since
+    # RCCL refuses two ranks on one GPU); timings are then not a scaling result
+    fa.set_device(int(os.environ.get("FFMI_BENCH_DEVICE", local)))
     comm = None
+    transport = "rccl"
+    mode_tp = os.environ.get("FFMI_TP_TRANSPORT", "xgmi")  # xgmi | rccl | xgmi-only
     if world > 1:
-        uid = ctrl.bcast(stdout_to_stderr(fa.Comm.unique_id) if rank == 0 else b"")
-        comm = stdout_to_stderr(lambda: fa.Comm(uid, world, rank))
+        if mode_tp == "xgmi-only":
+            comm = fa.Comm.peer(world, rank)
+        else:
+            uid = ctrl.bcast(stdout_to_stderr(fa.Comm.unique_id) if rank == 0 else b"")
+            comm = stdout_to_stderr(lambda: fa.Comm(uid, world, rank))
+        if mode_tp in ("xgmi", "xgmi-only"):
+            # the direct xGMI all-reduce: exchange buffers sized for the
+            # largest step's [T][H] fp16 partial, handles all-gathered here
+            hid = (fa.llama_config_from_hf(args.llm_weights) if args.llm_weights
+                   else LLAMA_7B)["hidden"]
+            cap_tokens = args.max_tokens_per_batch + 23 * args.batch + 16
+            try:
+                mine = comm.export(cap_tokens * hid * 2)
+            except Exception as e:  # noqa: BLE001 -- reported, then agreed on below
+                print(f"[bench] rank {rank}: xGMI export failed ({e})", file=sys.stderr)
+                mine = b""
+            handles = ctrl.allgather(mine)
+            ok = 0.0
+            if all(handles):  # every rank exported: attach (collective self-test)
+                try:
+                    comm.attach(handles)
+                    ok = 1.0
+                except Exception as e:  # noqa: BLE001
+                    print(f"[bench] rank {rank}: xGMI attach failed ({e})", file=sys.stderr)
+            if -ctrl.max(-ok) < 1.0:  # some rank failed: every rank stays on RCCL
+                if mode_tp == "xgmi-only":
+                    raise SystemExit("xGMI transport failed and FFMI_TP_TRANSPORT=xgmi-only")
+                comm.detach()
+            else:
+                transport = "xgmi"
 
     llm_cfg = fa.llama_config_from_hf(args.llm_weights) if args.llm_weights else dict(LLAMA_7B)
     ssm_cfg = fa.llama_config_from_hf(args.ssm_weights) if args.ssm_weights else dict(LLAMA_68M)
@@ -390,7 +449,8 @@ def main():
                    "ssm": ((f"LLaMA ({args.ssm_weights})" if args.ssm_weights
                             else "LLaMA-68M (random init)") if spec else None),
                    "global_batch": B, "prefill": P, "decode": D, "seq_len": max_len,
-                   "parallelism": f"tp{world}", "tree_widths": list(widths) if spec else None,
+                   "parallelism": f"tp{world}",
+                   "tp_transport": transport if world > 1 else None, "tree_widths": list(widths) if spec else None,
                    "max_tokens_per_batch": mtb, "layers": llm_cfg["num_layers"]},
         "p50_token_latency_ms": round(statistics.median(lats) / 1000.0, 3),
         "llm_steps_per_generate": llm_steps / args.steps,

@@ -16,6 +16,7 @@
 #include <climits>
 
 #include "ffmi_internal.h"
+#include "collective.h"
 
 static thread_local std::string g_last_error;
 
@@ -545,10 +546,29 @@ struct LocalGroup {
   }
 };
 
+// Direct xGMI transport (kernels/collective.hip): this rank's exchange buffer,
+// every peer's mapped through its IPC handle, and a host-mapped error word.
+struct PeerState {
+  size_t cap = 0;
+  char *own = nullptr;
+  char *base[ffmi::kMaxPeers] = {};
+  std::vector<void *> opened;
+  int *err_h = nullptr, *err_d = nullptr;
+  bool attached = false;
+  uint64_t timeout_ticks = 1000000000ull;  // 10 s at 100 MHz
+  size_t two_shot_min = 256 << 10;         // one-shot below (latency), two-shot above
+  ~PeerState() {
+    for (void *p : opened) (void)hipIpcCloseMemHandle(p);
+    if (own) (void)hipFree(own);
+    if (err_h) (void)hipHostFree(err_h);
+  }
+};
+
 struct ffmi_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0;
   std::shared_ptr<LocalGroup> local;
+  std::unique_ptr<PeerState> peer;
 };
 
 extern "C" ffmi_status ffmi_comm_create_local(int nranks, ffmi_comm **out) {
@@ -631,9 +651,194 @@ extern "C" void ffmi_comm_destroy(ffmi_comm *c) {
   delete c;
 }
 
+extern "C" ffmi_status ffmi_comm_create_peer(int nranks, int rank, ffmi_comm **out) {
+  FFMI_CHECK(out && nranks >= 1 && nranks <= ffmi::kMaxPeers && rank >= 0 && rank < nranks,
+             FFMI_ERR_INVALID);
+  ffmi_comm *c = new ffmi_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  *out = c;
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_comm_peer_export(ffmi_comm *c, size_t max_bytes, void *handle_out) {
+  FFMI_CHECK(c && handle_out && max_bytes > 0 && !c->local, FFMI_ERR_INVALID);
+  FFMI_CHECK(c->nranks <= ffmi::kMaxPeers && !c->peer, FFMI_ERR_INVALID);
+  static_assert(sizeof(hipIpcMemHandle_t) == FFMI_PEER_HANDLE_BYTES, "IPC handle size");
+  auto p = std::make_unique<PeerState>();
+  p->cap = (max_bytes + 255) & ~(size_t)255;
+  if (const char *e = getenv("FFMI_PEER_TIMEOUT_S")) p->timeout_ticks = (uint64_t)(atof(e) * 1e8);
+  // two ranks: two-shot moves the same bytes per rank as one-shot in two
+  // signal rounds, so one-shot at every size
+  if (c->nranks <= 2) p->two_shot_min = (size_t)-1;
+  if (const char *e = getenv("FFMI_PEER_TWO_SHOT_MIN")) p->two_shot_min = (size_t)atoll(e);
+  const size_t bytes = ffmi::peer_buffer_bytes(p->cap);
+  // uncached (MTYPE UC): every rank's loads of an exchange area reach memory,
+  // so a line read two epochs ago can never be served stale from an L2 --
+  // neither a peer's L2 over xGMI nor another XCD's L2 of this device (the
+  // multi-process test on one GPU).  FFMI_PEER_UNCACHED=0: plain hipMalloc +
+  // the system-scope fences alone (A/B).
+  const char *uc = getenv("FFMI_PEER_UNCACHED");
+  if (uc && !atoi(uc)) FFMI_HIP(hipMalloc((void **)&p->own, bytes));
+  else FFMI_HIP(hipExtMallocWithFlags((void **)&p->own, bytes, hipDeviceMallocUncached));
+  FFMI_HIP(hipMemset(p->own, 0, ffmi::kDataOff));  // inboxes, counters, epoch 0
+  FFMI_HIP(hipDeviceSynchronize());
+  FFMI_HIP(hipHostMalloc((void **)&p->err_h, sizeof(int), hipHostMallocMapped));
+  *p->err_h = 0;
+  FFMI_HIP(hipHostGetDevicePointer((void **)&p->err_d, p->err_h, 0));
+  hipIpcMemHandle_t h;
+  FFMI_HIP(hipIpcGetMemHandle(&h, p->own));
+  memcpy(handle_out, &h, sizeof(h));
+  c->peer = std::move(p);
+  return FFMI_OK;
+}
+
+static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows, size_t cols,
+                            size_t ld, size_t col0, int dtype, hipStream_t s) {
+  PeerState &p = *c->peer;
+  const size_t esz = dtype == FFMI_F16 ? 2 : 4;
+  const size_t bytes = rows * cols * esz;
+  FFMI_CHECK(bytes <= p.cap, FFMI_ERR_INVALID);
+  FFMI_CHECK((cols * esz) % 16 == 0 && ((size_t)in & 15) == 0 && ((size_t)out & 15) == 0 &&
+                 (ld * esz) % 16 == 0 && (col0 * esz) % 16 == 0,
+             FFMI_ERR_UNSUPPORTED);
+  ffmi::PeerArgs a;
+  for (int r = 0; r < ffmi::kMaxPeers; ++r) a.base[r] = p.base[r];
+  a.nranks = c->nranks;
+  a.rank = c->rank;
+  a.cap = p.cap;
+  a.in = in;
+  a.out = out;
+  a.nvec = bytes / 16;
+  a.vec_elems = 16 / esz;
+  a.cols = cols;
+  a.ld = ld;
+  a.col0 = col0;
+  a.esz = esz;
+  a.err = p.err_d;
+  a.timeout_ticks = p.timeout_ticks;
+  FFMI_HIP(ffmi::launch_peer_allreduce(a, bytes >= p.two_shot_min, s));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_comm_peer_status(ffmi_comm *c) {
+  FFMI_CHECK(c && c->peer, FFMI_ERR_INVALID);
+  if (*(volatile int *)c->peer->err_h != 0) {
+    ffmi_set_last_error(*(volatile int *)c->peer->err_h == 1
+                            ? "xGMI all-reduce: a peer never signalled (timeout, phase 1)"
+                            : "xGMI all-reduce: a peer never signalled (timeout, phase 2)",
+                        __FILE__, __LINE__);
+    return FFMI_ERR_NCCL;
+  }
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_comm_peer_attach(ffmi_comm *c, const void *handles) {
+  FFMI_CHECK(c && c->peer && handles && !c->peer->attached, FFMI_ERR_INVALID);
+  PeerState &p = *c->peer;
+  for (int r = 0; r < c->nranks; ++r) {
+    if (r == c->rank) {
+      p.base[r] = p.own;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    memcpy(&h, (const char *)handles + (size_t)r * FFMI_PEER_HANDLE_BYTES, sizeof(h));
+    void *ptr = nullptr;
+    FFMI_HIP(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+    p.opened.push_back(ptr);
+    p.base[r] = (char *)ptr;
+  }
+  // self-test (collective: every rank runs it): an exact f32 sum of small
+  // integers through both kernel variants, checked on the host
+  const int n = 4096 * c->nranks;
+  std::vector<float> h(n), got(n);
+  for (int i = 0; i < n; ++i) h[i] = (float)((c->rank + 1) * (i % 7));
+  float *d = nullptr;
+  FFMI_HIP(hipMalloc((void **)&d, (size_t)n * 4 * 2));
+  ffmi_status st = FFMI_OK;
+  p.attached = true;
+  for (int pass = 0; pass < 2 && st == FFMI_OK; ++pass) {
+    const size_t saved = p.two_shot_min;
+    p.two_shot_min = pass == 0 ? (size_t)-1 : 0;  // one-shot, then two-shot
+    if (hipMemcpy(d, h.data(), (size_t)n * 4, hipMemcpyHostToDevice) != hipSuccess) st = FFMI_ERR_HIP;
+    if (st == FFMI_OK) st = peer_run(c, d, d + n, 1, n, n, 0, FFMI_F32, nullptr);
+    if (st == FFMI_OK && hipDeviceSynchronize() != hipSuccess) st = FFMI_ERR_HIP;
+    if (st == FFMI_OK) st = ffmi_comm_peer_status(c);
+    if (st == FFMI_OK &&
+        hipMemcpy(got.data(), d + n, (size_t)n * 4, hipMemcpyDeviceToHost) != hipSuccess)
+      st = FFMI_ERR_HIP;
+    const float tri = 0.5f * c->nranks * (c->nranks + 1);
+    for (int i = 0; st == FFMI_OK && i < n; ++i)
+      if (got[i] != tri * (float)(i % 7)) {
+        ffmi_set_last_error("xGMI all-reduce self-test: wrong sum", __FILE__, __LINE__);
+        st = FFMI_ERR_NCCL;
+      }
+    p.two_shot_min = saved;
+  }
+  (void)hipFree(d);
+  if (st != FFMI_OK) p.attached = false;
+  return st;
+}
+
+extern "C" ffmi_status ffmi_comm_peer_detach(ffmi_comm *c) {
+  FFMI_CHECK(c, FFMI_ERR_INVALID);
+  if (c->peer) c->peer->attached = false;
+  return FFMI_OK;
+}
+
+namespace ffmi {
+bool comm_has_peer(const ffmi_comm *c, size_t bytes) {
+  return c && c->peer && c->peer->attached && bytes <= c->peer->cap;
+}
+int comm_size(const ffmi_comm *c) { return c ? c->nranks : 1; }
+ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
+                                int ld, int col0, int dtype, hipStream_t s) {
+  return peer_run(c, in, out, rows, cols, ld, col0, dtype, s);
+}
+ffmi_status comm_status(ffmi_comm *c) {
+  return c && c->peer && c->peer->attached ? ffmi_comm_peer_status(c) : FFMI_OK;
+}
+}  // namespace ffmi
+
+// Vocab-sharded softmax + argmax / arg-top-k (model.cc:3392-3419 Combine of
+// the vocab-parallel lm_head, then argmax.cu:62-100 / arg_topk.cu:339-448):
+// three record exchanges over the communicator (norm.hip vshard_kernel).
+static constexpr int kVshardW = 8;  // floats per (rank, row) record
+extern "C" size_t ffmi_vocab_shard_scratch_bytes(int nranks, int T) {
+  return nranks > 0 && T > 0 ? (size_t)nranks * T * kVshardW * sizeof(float) : 0;
+}
+
+extern "C" ffmi_status ffmi_vocab_shard_topk(ffmi_comm *c, const void *logits, int T, int Vl,
+                                             int k, int32_t *ids, float *probs, void *scratch,
+                                             ffmi_stream stream) {
+  FFMI_CHECK(c && logits && ids && scratch && T >= 0 && Vl > 0 && k >= 1 && k <= 4,
+             FFMI_ERR_INVALID);
+  FFMI_CHECK(c->nranks * kVshardW <= 256 && (size_t)c->rank * Vl + Vl <= 0x7fffffffu,
+             FFMI_ERR_UNSUPPORTED);
+  if (T == 0) return FFMI_OK;
+  const hipStream_t s = (hipStream_t)stream;
+  const int P = c->nranks;
+  float *x = (float *)scratch;
+  for (int phase = 0; phase < 3; ++phase) {
+    FFMI_HIP(ffmi::launch_vshard((const uint16_t *)logits, T, Vl, P, c->rank, k, phase, x,
+                                 kVshardW, nullptr, nullptr, s));
+    const ffmi_status st = ffmi_allreduce(c, x, x, (size_t)P * T * kVshardW, FFMI_F32, stream);
+    if (st != FFMI_OK) return st;
+  }
+  FFMI_HIP(ffmi::launch_vshard((const uint16_t *)logits, T, Vl, P, c->rank, k, 3, x, kVshardW,
+                               ids, probs, s));
+  return FFMI_OK;
+}
+
 extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
                                       int dtype, ffmi_stream stream) {
   FFMI_CHECK(c && in && out, FFMI_ERR_INVALID);
+  if (c->nranks > 1 && c->peer && c->peer->attached && dtype != FFMI_I32) {
+    const size_t esz = dtype == FFMI_F16 ? 2 : 4;
+    FFMI_CHECK(count * esz <= c->peer->cap, FFMI_ERR_INVALID);
+    return peer_run(c, in, out, 1, count, count, 0, dtype, (hipStream_t)stream);
+  }
+  FFMI_CHECK(c->local || c->comm || c->nranks == 1, FFMI_ERR_INVALID);
   if (c->local && c->nranks > 1)
     return local_allreduce(c, in, out, count, dtype, (hipStream_t)stream);
   if (c->nranks == 1) {

@@ -1,0 +1,43 @@
+// collective.h -- the direct xGMI all-reduce's exchange-buffer layout and
+// kernel arguments (kernels/collective.hip, api.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace ffmi {
+
+constexpr int kMaxPeers = 8;        // one node: the 8 GPUs of an MI355X platform
+// All-reduce grid cap.  Every workgroup may wait on a peer, so the whole
+// grid must be resident -- and it runs beside the GEMM of the other stream:
+// 32 workgroups (one per 8 CUs) keep ~1 MB of xGMI reads in flight and leave
+// the other CUs whole for the GEMM (a grid spread over every CU starves a
+// GEMM whose workgroups need a full CU's registers until the all-reduce ends)
+constexpr int kMaxPeerBlocks = 32;
+constexpr size_t kFlagStride = 256;  // one inbox slot per peer, own 256-B line
+// exchange buffer: [inbox0 8 slots][inbox1 8 slots][counters][data areas]
+constexpr size_t kInbox0 = 0;
+constexpr size_t kInbox1 = kMaxPeers * kFlagStride;
+constexpr size_t kHdrCounters = 2 * kMaxPeers * kFlagStride;
+constexpr int kCnt0 = 0, kCnt1 = 64, kCnt2 = 128, kEpochWord = 192;  // u32 words, 256-B apart
+constexpr size_t kDataOff = kHdrCounters + 4096;
+// data areas of `cap` bytes each: in[parity 0], in[parity 1], out[0], out[1]
+inline size_t peer_buffer_bytes(size_t cap) { return kDataOff + 4 * cap; }
+
+struct PeerArgs {
+  char *base[kMaxPeers];  // every rank's exchange buffer as mapped in this process
+  int nranks, rank;
+  size_t cap;             // bytes per data area
+  const void *in;         // [rows][cols] contiguous
+  void *out;              // row stride ld elements, starting at column col0
+  size_t nvec;            // 16-B vectors of the input
+  size_t vec_elems;       // elements per vector (8 f16 / 4 f32)
+  size_t cols, ld, col0;
+  size_t esz;
+  int *err;               // host-mapped error word (0 = ok)
+  uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+};
+
+hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s);
+
+}  // namespace ffmi

@@ -138,6 +138,11 @@ hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
                            size_t n, hipStream_t s);
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
                          float *probs, hipStream_t s);
+// Vocab-sharded tail (norm.hip): phase 0..2 write this rank's exchange
+// record ([P][T][W] floats, W >= max(4, 2k)); phase 3 merges into ids/probs.
+hipError_t launch_vshard(const uint16_t *logits, int T, int Vl, int P, int rank, int k,
+                         int phase, float *xch, int W, int32_t *ids, float *probs,
+                         hipStream_t s);
 hipError_t launch_group_sum(const void *const *bufs, int n, void *out, size_t count, int dtype,
                             hipStream_t s);
 
@@ -179,6 +184,16 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
 ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool record_event);
 // parity: which half of the TREE staging this step writes (commits read the
 // other); -1 = the handle's own alternation (public API calls)
+// Communicator internals for the model runtime (api.cpp): the direct xGMI
+// transport when attached and the message fits its buffers.
+bool comm_has_peer(const ffmi_comm *c, size_t bytes);
+int comm_size(const ffmi_comm *c);
+// sum of every rank's [rows][cols] `in` into `out` (row stride ld, starting
+// at column col0) over the xGMI transport
+ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
+                                int ld, int col0, int dtype, hipStream_t s);
+// FFMI_OK, or the transport's timeout error after a synchronised step
+ffmi_status comm_status(ffmi_comm *c);
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
                          void *out, ffmi_stream stream, int parity = -1);
 }  // namespace ffmi

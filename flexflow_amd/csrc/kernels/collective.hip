@@ -1,0 +1,219 @@
+// collective.hip -- direct xGMI all-reduce over peer exchange buffers.
+//
+// Replaces the reference's ncclAllReduce (allreduce_kernels.cu:53-75, run as
+// a concurrent Legion task per shard, allreduce.cc:291-331) for the
+// tensor-parallel LLaMA step.  Each rank owns one exchange buffer (uncached
+// device memory, exported with hipIpcGetMemHandle and mapped by every peer of
+// the node); a
+// single kernel per all-reduce does
+//   1. copy-in: this rank's partial -> its own exchange buffer (area `in`,
+//      parity e & 1 of the all-reduce epoch e);
+//   2. signal: the last workgroup to finish the copy pushes e into every
+//      rank's inbox slot for this rank (a system-scope release store over
+//      xGMI; its own slot too, for its own early workgroups), so every rank
+//      polls its LOCAL memory;
+//   3. one-shot (small messages): every rank reads all N partials and sums
+//      them in rank order 0..N-1 in fp32 -> bit-identical result on every
+//      rank;
+//      two-shot (large messages): rank r reduces chunk r of the vector
+//      (reading it from every peer), publishes it in its `out` area, signals
+//      again, then gathers the other chunks from their owners;
+//   4. the last workgroup to finish stores epoch e for the next launch.
+// The epoch lives in device memory, so the kernel's arguments are the same
+// on every launch and the whole step can be captured in a HIP graph.
+//
+// Reuse of the parity-p areas at epoch e + 2 is safe without extra flags:
+// a rank signals epoch e + 1 only after its all-reduce e has finished every
+// read of its peers' epoch-e areas (stream order), and it waits for every
+// peer's e + 1 signal before it writes a parity-p area again.
+//
+// Every wait is bounded (FFMI_PEER_TIMEOUT_S, default 10 s of s_memrealtime at
+// 100 MHz): a dead or missing peer sets the communicator's host-visible error
+// word and the kernel exits, so a broken exchange is an error, never a hang.
+//
+// All flag and counter stores are ordinary vector stores/atomics to global
+// memory.
+#include "../ffmi_internal.h"
+#include "../collective.h"
+
+namespace ffmi {
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ void report_timeout(int *err, int code) {
+  // host-mapped word (pinned), read after the step's stream synchronisation
+  __hip_atomic_store(err, code, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// All workgroups arrive; the last one (returns true) may act for the grid.
+__device__ __forceinline__ bool arrive_last(unsigned *cnt, unsigned G) {
+  __shared__ unsigned last;
+  __syncthreads();  // every wave of this workgroup has issued its stores
+  if (threadIdx.x == 0) {
+    // release at system scope: this workgroup's stores (its XCD's L2) are
+    // written back before the count moves; acquire: the last arriver sees
+    // every other workgroup's stores
+    const unsigned old =
+        __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_SYSTEM);
+    last = old == G - 1 ? 1u : 0u;
+    if (last) __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last != 0;
+}
+
+// Push epoch e into every rank's inbox slot for this rank -- this rank's own
+// slot included: the workgroups that arrived early must not read this rank's
+// area before its LAST workgroup has finished writing it.
+__device__ __forceinline__ void push_flags(const PeerArgs &a, size_t inbox_off, unsigned e) {
+  for (int p = 0; p < a.nranks; ++p) {
+    unsigned *f = reinterpret_cast<unsigned *>(a.base[p] + inbox_off + (size_t)a.rank * kFlagStride);
+    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+// Wait until every slot (every rank, this one included) of this rank's inbox
+// holds >= e.  Returns false on timeout (error word set).
+__device__ __forceinline__ bool wait_flags(const PeerArgs &a, size_t inbox_off, unsigned e,
+                                           int code) {
+  __shared__ int ok;
+  if (threadIdx.x == 0) ok = 1;
+  __syncthreads();
+  const int p = threadIdx.x;
+  if (p < a.nranks) {
+    const unsigned *f =
+        reinterpret_cast<const unsigned *>(a.base[a.rank] + inbox_off + (size_t)p * kFlagStride);
+    const uint64_t t0 = wall_clock64();
+    // peers are at most one epoch ahead (see the header), so >= e
+    while ((int)(__hip_atomic_load(f, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      __builtin_amdgcn_s_sleep(2);
+      if (wall_clock64() - t0 > a.timeout_ticks) {
+        report_timeout(a.err, code);
+        ok = 0;
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  // acquire (system scope: L1 and L2 invalidated): later loads of peer
+  // areas see what the peers released, not lines cached two epochs ago
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  return ok != 0;
+}
+
+template <int DT>  // 0: f16, 1: f32
+__device__ __forceinline__ void acc_vec(float (&acc)[8], uint4 v) {
+  if constexpr (DT == 0) {
+    const h8 h = __builtin_bit_cast(h8, v);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] += (float)h[i];
+  } else {
+    const f4 f = __builtin_bit_cast(f4, v);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i] += f[i];
+  }
+}
+
+template <int DT>
+__device__ __forceinline__ uint4 pack_vec(const float (&acc)[8]) {
+  if constexpr (DT == 0) {
+    h8 h;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = (_Float16)acc[i];
+    return __builtin_bit_cast(uint4, h);
+  } else {
+    f4 f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) f[i] = acc[i];
+    return __builtin_bit_cast(uint4, f);
+  }
+}
+
+// Vector v (16 B) of the logical [rows][cols] input -> its place in the
+// strided output (row stride ld elements, column offset col0).
+__device__ __forceinline__ uint4 *out_vec(const PeerArgs &a, size_t v) {
+  const size_t e = v * a.vec_elems;
+  const size_t row = e / a.cols, col = e % a.cols;
+  return reinterpret_cast<uint4 *>(reinterpret_cast<char *>(a.out) +
+                                   ((row * a.ld + a.col0 + col) * a.esz));
+}
+
+template <int DT, bool TWO_SHOT>
+__global__ __launch_bounds__(kThreads) void peer_allreduce_kernel(PeerArgs a) {
+  char *own = a.base[a.rank];
+  unsigned *hdr = reinterpret_cast<unsigned *>(own + kHdrCounters);
+  const unsigned e = hdr[kEpochWord] + 1u;  // written by the previous launch
+  const size_t par = e & 1u;
+  const size_t in_off = kDataOff + par * a.cap;
+  const size_t out_off = kDataOff + (2 + par) * a.cap;
+  const unsigned G = gridDim.x;
+  const size_t stride = (size_t)G * kThreads;
+  const size_t tid0 = (size_t)blockIdx.x * kThreads + threadIdx.x;
+
+  // 1. copy-in
+  {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.in);
+    uint4 *dst = reinterpret_cast<uint4 *>(own + in_off);
+    for (size_t v = tid0; v < a.nvec; v += stride) dst[v] = src[v];
+  }
+  // 2. signal
+  if (arrive_last(&hdr[kCnt0], G) && threadIdx.x == 0) push_flags(a, kInbox0, e);
+  if (!wait_flags(a, kInbox0, e, 1)) return;
+
+  if constexpr (!TWO_SHOT) {
+    // 3a. one-shot: every rank sums all N partials in rank order
+    for (size_t v = tid0; v < a.nvec; v += stride) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int p = 0; p < a.nranks; ++p)
+        acc_vec<DT>(acc, reinterpret_cast<const uint4 *>(a.base[p] + in_off)[v]);
+      *out_vec(a, v) = pack_vec<DT>(acc);
+    }
+  } else {
+    // 3b. two-shot: reduce my chunk, publish, gather the others
+    const size_t c0 = a.nvec * a.rank / a.nranks, c1 = a.nvec * (a.rank + 1) / a.nranks;
+    uint4 *pub = reinterpret_cast<uint4 *>(own + out_off);
+    for (size_t v = c0 + tid0; v < c1; v += stride) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+      for (int p = 0; p < a.nranks; ++p)
+        acc_vec<DT>(acc, reinterpret_cast<const uint4 *>(a.base[p] + in_off)[v]);
+      const uint4 r = pack_vec<DT>(acc);
+      pub[v] = r;
+      *out_vec(a, v) = r;
+    }
+    if (arrive_last(&hdr[kCnt1], G) && threadIdx.x == 0) push_flags(a, kInbox1, e);
+    if (!wait_flags(a, kInbox1, e, 2)) return;
+    for (int q = 1; q < a.nranks; ++q) {
+      const int p = (a.rank + q) % a.nranks;  // spread the first reads over the links
+      const size_t p0 = a.nvec * p / a.nranks, p1 = a.nvec * (p + 1) / a.nranks;
+      const uint4 *src = reinterpret_cast<const uint4 *>(a.base[p] + out_off);
+      for (size_t v = p0 + tid0; v < p1; v += stride) *out_vec(a, v) = src[v];
+    }
+  }
+  // 4. the epoch of the next launch
+  if (arrive_last(&hdr[kCnt2], G) && threadIdx.x == 0)
+    __hip_atomic_store(&hdr[kEpochWord], e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace
+
+hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s) {
+  if (a.nvec == 0) return hipSuccess;
+  // enough workgroups to keep xGMI reads in flight, few enough to be
+  // co-resident with the GEMMs of a concurrent stream (every workgroup may
+  // wait on a peer, so the whole grid must be resident)
+  size_t per = two_shot ? (a.nvec + a.nranks - 1) / a.nranks : a.nvec;
+  unsigned G = (unsigned)std::min<size_t>(kMaxPeerBlocks, (per + kThreads - 1) / kThreads);
+  if (G == 0) G = 1;
+  if (a.esz == 2) {
+    if (two_shot) hipLaunchKernelGGL((peer_allreduce_kernel<0, true>), dim3(G), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((peer_allreduce_kernel<0, false>), dim3(G), dim3(kThreads), 0, s, a);
+  } else {
+    if (two_shot) hipLaunchKernelGGL((peer_allreduce_kernel<1, true>), dim3(G), dim3(kThreads), 0, s, a);
+    else hipLaunchKernelGGL((peer_allreduce_kernel<1, false>), dim3(G), dim3(kThreads), 0, s, a);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace ffmi

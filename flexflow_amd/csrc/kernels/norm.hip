@@ -457,6 +457,155 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Vocab-sharded greedy / speculative tail (model.cc:3392-3419 shards lm_head
+// over the vocabulary and Combines; here every rank keeps its [T][V/P] logit
+// shard and three small exchanges of per-row records make the pick global):
+//   phase 0: local max m_r                     -> exchange -> M = max_r m_r
+//   phase 1: local sum of exp(x - M) (double)  -> exchange -> S = float(sum)
+//   phase 2: local top-k of p = half(exp(x-M)/S) (p desc, lowest global id)
+//            -> exchange -> merge: the k best of the P*k candidates.
+// M and S are the unsharded kernel's values (a max is exact; S is the float
+// rounding of the same double sum, accumulated per shard then over ranks in
+// rank order), and p is computed with the same expressions, so the pick and
+// its tie rule (lowest index of the largest fp16 p, cub ArgMax / the top-k
+// heap) are those of the one-GPU kernel.  Exchange records are [P][T][W]
+// floats: a rank writes its own slot and zeroes the others, and the sum
+// all-reduce then acts as an all-gather (x + 0 = x).
+// ---------------------------------------------------------------------------
+template <int TPB>
+__device__ __forceinline__ float block_max(float v, float *sh) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float m = sh[0];
+#pragma unroll
+  for (int q = 1; q < TPB / 64; ++q) m = fmaxf(m, sh[q]);
+  __syncthreads();
+  return m;
+}
+
+template <int TPB>
+__global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict__ logits, int T,
+                                                      int Vl, int P, int rank, int k, int phase,
+                                                      float *__restrict__ xch, int W,
+                                                      int32_t *__restrict__ ids,
+                                                      float *__restrict__ probs) {
+  __shared__ double dsh[TPB / 64];
+  __shared__ float fsh[TPB / 64];
+  __shared__ unsigned long long ksh[TPB / 64];
+  const int t = blockIdx.x, tid = threadIdx.x;
+  const uint16_t *x = logits + (size_t)t * Vl;
+  auto slot = [&](int r) { return xch + ((size_t)r * T + t) * W; };
+  if (phase == 3) {  // merge the P*k candidates of the last exchange
+    if (tid == 0) {
+      int taken[4] = {-1, -1, -1, -1};
+      for (int rd = 0; rd < k; ++rd) {
+        unsigned long long best = 0;
+        int bq = -1;
+        for (int r = 0; r < P; ++r)
+          for (int j = 0; j < k; ++j) {
+            const float pv = slot(r)[2 * j], iv = slot(r)[2 * j + 1];
+            if (iv < 0.f) continue;  // (empty candidate)
+            const int q = r * k + j;
+            bool used = false;
+            for (int z = 0; z < rd; ++z) used |= taken[z] == q;
+            if (used) continue;
+            const unsigned long long key =
+                ((unsigned long long)(f2h_(pv) + 1u) << 32) |
+                (unsigned long long)(0xffffffffu - (unsigned)iv);
+            if (key > best) best = key, bq = q;
+          }
+        taken[rd] = bq;
+        ids[(size_t)t * k + rd] = (int)(0xffffffffu - (unsigned)(best & 0xffffffffu));
+        if (probs) probs[(size_t)t * k + rd] = h2f_((uint16_t)((best >> 32) - 1u));
+      }
+    }
+    return;
+  }
+  float *own = slot(rank);
+  if (phase == 0) {
+    float m = -INFINITY;
+    for (int i = tid; i < Vl; i += TPB) m = fmaxf(m, h2f_(x[i]));
+    m = block_max<TPB>(m, fsh);
+    if (tid < P * W) {
+      const int r = tid / W, w = tid % W;
+      slot(r)[w] = (r == rank && w == 0) ? m : 0.f;
+    }
+    return;
+  }
+  float M = -INFINITY;
+  for (int r = 0; r < P; ++r) M = fmaxf(M, xch[((size_t)r * T + t) * W]);  // phase-0 records
+  if (phase == 1) {
+    // (exchange buffer: [P][T][W] of phase 0 is read above and rewritten
+    //  below only after the whole block has read it)
+    double se = 0.0;
+    for (int i = tid; i < Vl; i += TPB) se += (double)__expf(h2f_(x[i]) - M);
+    se = block_sum256(se, dsh);
+    __syncthreads();
+    if (tid < P * W) {
+      const int r = tid / W, w = tid % W;
+      const float hi = (float)se, lo = (float)(se - (double)hi);
+      slot(r)[w] = r != rank ? 0.f : (w == 0 ? M : w == 1 ? hi : w == 2 ? lo : 0.f);
+    }
+    return;
+  }
+  // phase 2: global S from the phase-1 records, local top-k candidates
+  double sd = 0.0;
+  for (int r = 0; r < P; ++r) {
+    const float *q = xch + ((size_t)r * T + t) * W;
+    sd += (double)q[1] + (double)q[2];
+  }
+  const float S = (float)sd;
+  __syncthreads();  // every thread has read the phase-1 records
+  int chosen[4] = {-1, -1, -1, -1};
+  for (int rd = 0; rd < k; ++rd) {
+    unsigned long long best = 0;
+    for (int i = tid; i < Vl; i += TPB) {
+      bool used = false;
+      for (int z = 0; z < rd; ++z) used |= chosen[z] == i;
+      if (used) continue;
+      const uint16_t p = f2h_(__fdiv_rn(expf(h2f_(x[i]) - M), S));
+      const unsigned gi = (unsigned)(rank * Vl + i);
+      const unsigned long long key =
+          ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - gi);
+      best = key > best ? key : best;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const unsigned long long ot = __shfl_xor(best, o);
+      best = ot > best ? ot : best;
+    }
+    if ((tid & 63) == 0) ksh[tid >> 6] = best;
+    __syncthreads();
+    unsigned long long b = ksh[0];
+#pragma unroll
+    for (int q = 1; q < TPB / 64; ++q) b = ksh[q] > b ? ksh[q] : b;
+    __syncthreads();
+    chosen[rd] = b ? (int)(0xffffffffu - (unsigned)(b & 0xffffffffu)) - rank * Vl : -1;
+    if (tid == 0) {
+      own[2 * rd] = b ? h2f_((uint16_t)((b >> 32) - 1u)) : 0.f;
+      own[2 * rd + 1] = b ? (float)(0xffffffffu - (unsigned)(b & 0xffffffffu)) : -1.f;
+    }
+  }
+  if (tid < P * W) {  // zero the other ranks' slots and this slot's unused tail
+    const int r = tid / W, w = tid % W;
+    if (r != rank) slot(r)[w] = 0.f;
+    else if (w >= 2 * k) own[w] = 0.f;
+  }
+}
+
+hipError_t launch_vshard(const uint16_t *logits, int T, int Vl, int P, int rank, int k,
+                         int phase, float *xch, int W, int32_t *ids, float *probs,
+                         hipStream_t s) {
+  if (T <= 0) return hipSuccess;
+  if (k < 1 || k > 4 || P * W > 256 || W < 2 * k || W < 4) return hipErrorInvalidValue;
+  hipLaunchKernelGGL((vshard_kernel<256>), dim3(T), dim3(256), 0, s, logits, T, Vl, P, rank, k,
+                     phase, xch, W, ids, probs);
+  return hipGetLastError();
+}
+
 // Sum of the ranks' buffers of an in-process shard group (ffmi_comm_create_
 // local): out = sum over r in rank order, fp16 accumulated in fp32 then
 // rounded once (RCCL's ring sums in fp16 in ring order; both are within an

@@ -53,6 +53,20 @@ struct LlamaGPU : public ffmi_model {
   uint16_t *res = nullptr, *h = nullptr, *qkv = nullptr, *att = nullptr, *proj = nullptr,
            *mlp = nullptr, *logits = nullptr;
   int32_t *ids_d = nullptr;
+  // vocab-sharded lm_head at TP > 1 (model.cc:3392-3419): this rank's Vl rows
+  // and the [P][Tm][kXW] exchange records of the sharded softmax / top-k
+  int Vl = 0;
+  float *xch = nullptr;
+  // TP over the direct xGMI transport (ffmi_comm_peer_attach): the
+  // row-parallel GEMMs run in two column halves; each half is all-reduced on
+  // comm_stream while the next half computes (allreduce.cc:291-331 runs the
+  // collective as a concurrent task; here it overlaps on HIP streams)
+  bool peer = false;
+  int tp_chunks = 1;
+  hipStream_t comm_stream = nullptr;
+  uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
+  std::vector<hipEvent_t> ev_chunk;
+  hipEvent_t ev_comm_done = nullptr;
   float *ws = nullptr;  // split-K workspace of the GEMMs
   size_t ws_bytes = 0;
   int32_t *ids_h = nullptr;
@@ -139,7 +153,7 @@ struct LlamaGPU : public ffmi_model {
   int op_stats(ffmi_op_stat *out, int cap) override {
     static const char *names[NCAT] = {"gemm_qkv", "gemm_o_proj", "gemm_gate_up_silu",
                                       "gemm_down", "gemm_lm_head", "attention", "rmsnorm",
-                                      "allreduce", "softmax_argmax", "embedding"};
+                                      "rowpar_gemm_allreduce", "softmax_argmax", "embedding"};
     int n = 0;
     for (int i = 0; i < NCAT; ++i) {
       if (opstat[i].launches == 0) continue;
@@ -187,8 +201,8 @@ struct LlamaGPU : public ffmi_model {
   }
   long debug_tensor(int which, int layer, float *out, long cap) override {
     if (dbg_T < 0 || (stream && hipStreamSynchronize(stream) != hipSuccess)) return -1;
-    const int T = dbg_T, H = c.hidden, V = c.vocab_size;
-    const int width = which == FFMI_DBG_LOGITS ? V : H;
+    const int T = dbg_T, H = c.hidden;
+    const int width = which == FFMI_DBG_LOGITS ? Vl : H;  // (this rank's vocab shard)
     if ((which != FFMI_DBG_LOGITS && which != FFMI_DBG_HIDDEN) ||
         (which == FFMI_DBG_HIDDEN && (layer < 0 || layer > c.num_layers)) ||
         cap < (long)T * width)
@@ -215,6 +229,9 @@ struct LlamaGPU : public ffmi_model {
     clear_graphs();
     for (auto &L : layers) ffmi_attn_destroy(L.attn);
     for (auto e : ev_pool) (void)hipEventDestroy(e);
+    for (auto e : ev_chunk) (void)hipEventDestroy(e);
+    if (ev_comm_done) (void)hipEventDestroy(ev_comm_done);
+    if (comm_stream) (void)hipStreamDestroy(comm_stream);
     for (void *p : allocs) (void)hipFree(p);
     if (ids_h) (void)hipHostFree(ids_h);
     ffmi_batch_destroy(batch);
@@ -315,8 +332,23 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&att, (size_t)Tm * Hl));
     TRY(alloc(&proj, (size_t)Tm * H));
     TRY(alloc(&mlp, (size_t)Tm * Fl));
-    TRY(alloc(&logits, (size_t)Tm * V));
+    Vl = P > 1 && V % P == 0 && (V / P) % 16 == 0 ? V / P : V;
+    if (const char *e = getenv("FFMI_VOCAB_SHARD"))  // A/B: 0 = replicated lm_head
+      if (!atoi(e)) Vl = V;
+    TRY(alloc(&logits, (size_t)Tm * Vl));
+    if (Vl != V) TRY(alloc(&xch, (ffmi_vocab_shard_scratch_bytes(P, Tm) + 3) / 4));
     TRY(alloc(&ids_d, (size_t)Tm * 4 * 2));  // [ids | probs] of a step, one D2H copy
+    peer = P > 1 && ffmi::comm_has_peer(o.comm, (size_t)Tm * H * 2);
+    if (peer) {
+      tp_chunks = 2;
+      if (const char *e = getenv("FFMI_TP_OVERLAP")) tp_chunks = atoi(e) ? 2 : 1;
+      if ((H / tp_chunks) % 32 != 0) tp_chunks = 1;
+      FFMI_HIP(hipStreamCreateWithFlags(&comm_stream, hipStreamNonBlocking));
+      ev_chunk.resize(tp_chunks);
+      for (auto &e : ev_chunk) FFMI_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      FFMI_HIP(hipEventCreateWithFlags(&ev_comm_done, hipEventDisableTiming));
+      if (tp_chunks > 1) TRY(alloc(&chunk_buf, (size_t)Tm * H));
+    }
     {
       // the split-K factor depends on the row-block count, so take the max
       // over every batch size the model can see
@@ -325,7 +357,7 @@ struct LlamaGPU : public ffmi_model {
         const size_t w2 = ffmi_linear_workspace_bytes(t, H, Hl, FFMI_EPI_NONE);
         const size_t w3 = ffmi_linear_workspace_bytes(t, Fl, H, FFMI_EPI_SILU_MUL);
         const size_t w4 = ffmi_linear_workspace_bytes(t, H, Fl, FFMI_EPI_NONE);
-        const size_t w5 = ffmi_linear_workspace_bytes(t, V, H, FFMI_EPI_NONE);
+        const size_t w5 = ffmi_linear_workspace_bytes(t, Vl, H, FFMI_EPI_NONE);
         ws_bytes = std::max(ws_bytes, std::max(std::max(std::max(w1, w2), std::max(w3, w4)), w5));
       }
       if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
@@ -343,9 +375,10 @@ struct LlamaGPU : public ffmi_model {
     TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0));
     TRY(alloc(&final_norm, H));
     TRY(fill(final_norm, H, "model.norm.weight", 1));
-    TRY(alloc(&lm, ffmi_linear_packed_bytes(V, H) / 2));
+    TRY(alloc(&lm, ffmi_linear_packed_bytes(Vl, H) / 2));
     TRY(fill(tmp, (size_t)V * H, "lm_head.weight", 0));
-    FFMI_HIP(launch_pack_weight(tmp, H, 0, 0, V, H, lm, 0, 0, stream));
+    // vocab shard s: rows [s*Vl, (s+1)*Vl) (the whole table when replicated)
+    FFMI_HIP(launch_pack_weight(tmp, H, Vl == V ? 0 : o.tp_rank * Vl, 0, Vl, H, lm, 0, 0, stream));
     slots = 0;
     layers.resize(c.num_layers);
     const int s = o.tp_rank;
@@ -419,6 +452,35 @@ struct LlamaGPU : public ffmi_model {
     return ffmi_allreduce(o.comm, buf, buf, n, FFMI_F16, (ffmi_stream)stream);
   }
 
+  // Row-parallel GEMM + sum all-reduce into `out` [T][H] (model.cc:3421-3445).
+  // Over the xGMI transport the output columns are computed in tp_chunks
+  // halves: half c goes to comm_stream for its all-reduce (strided into
+  // `out`) as soon as its GEMM is done, while half c + 1 computes.
+  ffmi_status rowpar_gemm_allreduce(const uint16_t *X, const uint16_t *W, int K, uint16_t *out,
+                                    int T, int XP) {
+    const int H = c.hidden;
+    if (!peer || tp_chunks == 1) {
+      FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream, nullptr));
+      if (peer) return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream);
+      return allreduce(out, (size_t)T * H);
+    }
+    const int Hc = H / tp_chunks;
+    const size_t tiles = (size_t)(Hc / 16) * ((K + 31) / 32) * 512;  // packed rows of a chunk
+    for (int ch = 0; ch < tp_chunks; ++ch) {
+      uint16_t *cb = chunk_buf + (size_t)ch * T * Hc;
+      FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb, ws, ws_bytes, T, Hc, K, XP, stream,
+                                 nullptr));
+      FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
+      FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
+      ffmi_status st =
+          ffmi::comm_allreduce_cols(o.comm, cb, out, T, Hc, H, ch * Hc, FFMI_F16, comm_stream);
+      if (st != FFMI_OK) return st;
+    }
+    FFMI_HIP(hipEventRecord(ev_comm_done, comm_stream));
+    FFMI_HIP(hipStreamWaitEvent(stream, ev_comm_done, 0));
+    return FFMI_OK;
+  }
+
   // One step over the packed batch; k = results per token.  Small batches
   // (SSM beam steps, decode) are launch-bound -- ~20 kernels of a few us
   // each -- so their whole step (metadata copy, kernels, result copies) is
@@ -454,7 +516,8 @@ struct LlamaGPU : public ffmi_model {
     // request (a fixed shape while the batch is full: T = 168 for 8 requests
     // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
     const bool graph = use_graphs && !dbg && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
-                       o.tp_size == 1 && !prof_on(0, T) && !prof_on(c.num_layers / 2, T);
+                       (o.tp_size == 1 || peer) && !prof_on(0, T) &&
+                       !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
                          batch->commit_overlap ? 1 : 0, batch->one_item_per_req ? 1 : 0,
@@ -483,6 +546,7 @@ struct LlamaGPU : public ffmi_model {
       if (st != FFMI_OK) return st;
     }
     FFMI_HIP(hipStreamSynchronize(stream));
+    if (peer && (st = ffmi::comm_status(o.comm)) != FFMI_OK) return st;
     if (mode == FFMI_MODEL_TREE) tree_parity ^= 1;
     if (!recs.empty()) prof_collect();
     return FFMI_OK;
@@ -533,14 +597,17 @@ struct LlamaGPU : public ffmi_model {
       TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s,
                              mode == FFMI_MODEL_TREE ? tree_parity : -1));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
-      pr = prof_begin(on);
       ffmi::Partials o_part;
-      FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
-                                 o.tp_size == 1 && H <= 8192 ? &o_part : nullptr));
-      prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
-      pr = prof_begin(on && o.tp_size > 1);
-      TRY(allreduce(proj, (size_t)T * H));
-      prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
+      if (o.tp_size == 1) {
+        pr = prof_begin(on);
+        FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
+                                   H <= 8192 ? &o_part : nullptr));
+        prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+      } else {  // GEMM + all-reduce (overlapped over xGMI): timed together
+        pr = prof_begin(on);
+        TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
+        prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+      }
       pr = prof_begin(on);
       FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
                                     o_part));
@@ -549,13 +616,16 @@ struct LlamaGPU : public ffmi_model {
       const int YP = packed ? FFMI_Y_PACKED : 0;
       TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
-      pr = prof_begin(on);
-      FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
-                                 o.tp_size == 1 && H <= 8192 ? &down_part : nullptr));
-      prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
-      pr = prof_begin(on && o.tp_size > 1);
-      TRY(allreduce(proj, (size_t)T * H));
-      prof_end(pr, ALLREDUCE, (double)T * H * 2, 0);
+      if (o.tp_size == 1) {
+        pr = prof_begin(on);
+        FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
+                                   H <= 8192 ? &down_part : nullptr));
+        prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+      } else {
+        pr = prof_begin(on);
+        TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
+        prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+      }
     }
     const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
     pr = prof_begin(ptail);
@@ -572,8 +642,8 @@ struct LlamaGPU : public ffmi_model {
       dbg_T = T;
     }
     pr = prof_begin(ptail);
-    TRY(ffmi_linear_ws(h, lm, logits, T, V, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
-    prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, V, V, H), 2.0 * T * V * H);
+    TRY(ffmi_linear_ws(h, lm, logits, T, Vl, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
+    prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, Vl, Vl, H), 2.0 * T * Vl * H);
     pr = prof_begin(ptail);
     // ids [T*k] then probs [T*k] back to back.  The sampling kernel writes
     // them straight into the pinned host buffer (a few bytes per row over
@@ -582,10 +652,14 @@ struct LlamaGPU : public ffmi_model {
     // keeps the device buffer + copy (A/B runs)
     int32_t *ids_o = result_copy ? ids_d : ids_h;
     float *probs_o = reinterpret_cast<float *>(ids_o + (size_t)T * k);
-    if (k == 1)
+    if (Vl != V) {
+      // sharded softmax / top-k: three record exchanges, then the merge
+      TRY(ffmi_vocab_shard_topk(o.comm, logits, T, Vl, k, ids_o, probs_o, xch, s));
+    } else if (k == 1) {
       TRY(ffmi_argmax(logits, T, V, ids_o, probs_o, s));
-    else
+    } else {
       TRY(ffmi_arg_topk(logits, T, V, k, ids_o, probs_o, s));
+    }
     prof_end(pr, SAMPLING, (double)T * V * 2, 0);
     if (result_copy)
       FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));

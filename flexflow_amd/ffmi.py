@@ -137,6 +137,14 @@ SIGNATURES = {
     "ffmi_comm_create": (c_int, [c_void_p, c_int, c_int, ctypes.POINTER(c_void_p)]),
     "ffmi_comm_create_local": (c_int, [c_int, ctypes.POINTER(c_void_p)]),
     "ffmi_comm_destroy": (None, [c_void_p]),
+    "ffmi_comm_create_peer": (c_int, [c_int, c_int, ctypes.POINTER(c_void_p)]),
+    "ffmi_comm_peer_export": (c_int, [c_void_p, c_size_t, c_void_p]),
+    "ffmi_comm_peer_attach": (c_int, [c_void_p, c_void_p]),
+    "ffmi_comm_peer_status": (c_int, [c_void_p]),
+    "ffmi_comm_peer_detach": (c_int, [c_void_p]),
+    "ffmi_vocab_shard_scratch_bytes": (c_size_t, [c_int, c_int]),
+    "ffmi_vocab_shard_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
+                                      c_void_p, c_void_p, c_void_p]),
     "ffmi_allreduce": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
     "ffmi_embedding": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "ffmi_silu_mul": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),

@@ -116,6 +116,37 @@ class Comm:
             out.append(c)
         return out
 
+    @classmethod
+    def peer(cls, nranks: int, rank: int):
+        """A communicator with the direct xGMI transport only (no RCCL
+        state): export() its exchange buffer, all-gather the handles over the
+        caller's control plane, then attach() them (ffmi_comm_create_peer)."""
+        c = cls.__new__(cls)
+        h = ctypes.c_void_p()
+        F.check(F.lib().ffmi_comm_create_peer(nranks, rank, ctypes.byref(h)), "peer comm")
+        c.handle = h
+        return c
+
+    def export(self, max_bytes: int) -> bytes:
+        """Allocate this rank's exchange buffer (4 x max_bytes) and return its
+        64-byte IPC handle (ffmi_comm_peer_export)."""
+        buf = ctypes.create_string_buffer(64)
+        F.check(F.lib().ffmi_comm_peer_export(self.handle, max_bytes, buf), "peer export")
+        return buf.raw
+
+    def attach(self, handles) -> None:
+        """Map every rank's exchange buffer (handles in rank order) and run the
+        collective self-test (ffmi_comm_peer_attach)."""
+        blob = b"".join(handles)
+        buf = ctypes.create_string_buffer(blob, len(blob))
+        F.check(F.lib().ffmi_comm_peer_attach(self.handle, buf), "peer attach")
+
+    def detach(self) -> None:
+        F.check(F.lib().ffmi_comm_peer_detach(self.handle), "peer detach")
+
+    def status(self) -> None:
+        F.check(F.lib().ffmi_comm_peer_status(self.handle), "peer status")
+
     def close(self):
         if getattr(self, "handle", None):
             F.lib().ffmi_comm_destroy(self.handle)

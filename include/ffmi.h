@@ -225,6 +225,44 @@ void ffmi_comm_destroy(ffmi_comm *c);
 ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, size_t count,
                            int dtype, ffmi_stream stream);
 
+/* Direct xGMI transport (replaces the NCCL data path of the same wrapper,
+ * allreduce_kernels.cu:53-75, for a node's ranks).  Every rank exports one
+ * exchange buffer of 4 x max_bytes (+ a 20 KiB header) as an IPC handle; the
+ * caller's control plane all-gathers the handles ([nranks][64 B], rank
+ * order) and every rank attaches them.  ffmi_allreduce on such a
+ * communicator then runs ONE kernel per call: copy-in, a flag pushed into
+ * each peer's memory, and a one-shot (every rank sums all partials) or
+ * two-shot (reduce-scatter + all-gather through the peers' buffers) sum in
+ * rank order -- bit-identical on every rank, graph-capturable (the epoch is
+ * device-resident), never hanging (a peer silent for FFMI_PEER_TIMEOUT_S,
+ * default 10, sets an error that ffmi_comm_peer_status reports).  Attach is
+ * collective and ends with a checked self-test all-reduce.
+ * ffmi_comm_create_peer makes a communicator with no RCCL state (the
+ * transport alone: also what the multi-process tests on one GPU use). */
+/* Vocab-parallel greedy / speculative tail (replaces the reference's
+ * vocab-sharded lm_head + Combine, model.cc:3392-3419 / combine.cc:200-262,
+ * followed by Softmax + ArgMax / ArgTopK, softmax.cu:262-288, argmax.cu:62-100,
+ * arg_topk.cu:339-448).  Each rank holds logits [T][Vl] for vocabulary ids
+ * [rank*Vl, (rank+1)*Vl); every rank gets the GLOBAL k best ids (k <= 4) and
+ * their fp16 softmax probabilities, identical to ffmi_arg_topk on the
+ * gathered [T][P*Vl] logits (same max, same float rounding of the same
+ * double sum, lowest index among equal fp16 probabilities).  Three
+ * exchanges of (P x T x 32 B) records over the communicator; `scratch` holds
+ * ffmi_vocab_shard_scratch_bytes(P, T) device bytes. */
+size_t ffmi_vocab_shard_scratch_bytes(int nranks, int T);
+ffmi_status ffmi_vocab_shard_topk(ffmi_comm *c, const void *logits, int T, int Vl, int k,
+                                  int32_t *ids, float *probs, void *scratch, ffmi_stream stream);
+
+#define FFMI_PEER_HANDLE_BYTES 64
+ffmi_status ffmi_comm_create_peer(int nranks, int rank, ffmi_comm **out);
+ffmi_status ffmi_comm_peer_export(ffmi_comm *c, size_t max_bytes,
+                                  void *handle_out /* FFMI_PEER_HANDLE_BYTES */);
+ffmi_status ffmi_comm_peer_attach(ffmi_comm *c, const void *handles /* [nranks][64] */);
+ffmi_status ffmi_comm_peer_status(ffmi_comm *c);
+/* Stop using the transport (RCCL again): for a control plane that saw some
+ * rank fail its attach -- every rank must take the same transport. */
+ffmi_status ffmi_comm_peer_detach(ffmi_comm *c);
+
 /* ------------------------------------------------------------------------ */
 /* Auxiliary ops on the LLaMA greedy path                                    */
 /* ------------------------------------------------------------------------ */

@@ -1,0 +1,114 @@
+"""Rank tasks for tests/peer_group.py (run inside the spawned rank processes)."""
+import time
+
+import numpy as np
+
+
+def case_data(case, it, rank, count, dtype):
+    rng = np.random.default_rng(1000003 * case + 7919 * it + rank)
+    x = rng.standard_normal(count).astype(np.float32)
+    return x.astype(np.float16) if dtype == "f16" else x
+
+
+def ar_task(fa, comm, rank, n, cases, iters):
+    """ffmi_allreduce over the xGMI transport, `iters` back-to-back rounds of
+    every case (epochs, parities and buffer reuse all cycle)."""
+    import flexflow_amd.ffmi as F
+    from hip_util import Buf, sync
+    L = F.lib()
+    out = {}
+    for it in range(iters):
+        for ci, (count, dtype) in enumerate(cases):
+            x = case_data(ci, it, rank, count, dtype)
+            src = Buf(x)
+            dst = Buf.empty(x.shape, x.dtype)
+            F.check(L.ffmi_allreduce(comm.handle, src.ptr, dst.ptr, count,
+                                     F.F16 if dtype == "f16" else F.F32, None), "allreduce")
+            sync()
+            out[(it, ci)] = dst.get()
+    return out
+
+
+def expected_sum(case, it, n, count, dtype):
+    acc = np.zeros(count, np.float32)
+    for r in range(n):  # rank order, fp32, rounded once
+        acc = acc + case_data(case, it, r, count, dtype).astype(np.float32)
+    return acc.astype(np.float16) if dtype == "f16" else acc
+
+
+def silent_peer_task(fa, comm, rank, n):
+    """Rank 0 all-reduces alone: its kernel must time out and report it."""
+    import flexflow_amd.ffmi as F
+    from hip_util import Buf, sync
+    if rank != 0:
+        time.sleep(4)  # keep the buffer mapped while rank 0 waits
+        return "idle"
+    x = Buf(np.ones(4096, np.float32))
+    t0 = time.time()
+    F.check(F.lib().ffmi_allreduce(comm.handle, x.ptr, x.ptr, 4096, F.F32, None), "allreduce")
+    sync()
+    dt = time.time() - t0
+    st = F.lib().ffmi_comm_peer_status(comm.handle)
+    comm.expect_error = True  # (the harness's final status check is skipped)
+    return {"status": int(st), "seconds": dt,
+            "msg": F.lib().ffmi_last_error().decode(errors="replace")}
+
+
+def model_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ssm_cfg):
+    """One TP shard of a LLaMA model per rank, over the xGMI transport."""
+    mode = "tree" if spec else "inc"
+    extra = 23 * 4 if spec else 0
+    m = fa.Model(cfg, mode, max_requests=4, max_tokens=32 + extra, max_seq_len=128,
+                 weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm)
+    rm = fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=32,
+                           max_sequence_length=128, spec_tree_width=(1, 1, 3) if spec else ())
+    if spec:
+        rm.register_ssm_model(fa.Model(ssm_cfg, "beam", max_requests=4, max_tokens=32 + extra,
+                                       max_seq_len=128, weight_seed=5))
+    res = fa.generate(rm, m, prompts, max_length=max_length)
+    m.close()
+    return [r.output_tokens for r in res]
+
+
+def planted_logits(T, V, seed):
+    """Logit rows with planted cross-shard ties: equal maxima in different
+    shards, rows of near-equal logits whose fp16 probabilities tie, random
+    rows."""
+    rng = np.random.default_rng(seed)
+    x = rng.standard_normal((T, V)).astype(np.float32) * 3
+    for t in range(T):
+        kind = t % 4
+        if kind == 0:  # the same maximum at several ids across shards
+            m = x[t].max() + 1.0
+            for i in rng.choice(V, 4, replace=False):
+                x[t, i] = m
+        elif kind == 1:  # tiny spread: the fp16 softmax rounds many ids to one p
+            x[t] = rng.choice([0.0, 2.0 ** -14, 2.0 ** -13, 2.0 ** -12], V)
+        elif kind == 2:  # second-best equal to best after rounding, other shard
+            i, j = rng.choice(V, 2, replace=False)
+            x[t, i] = x[t].max() + 2.0
+            x[t, j] = x[t, i] - 2.0 ** -9
+    return x.astype(np.float16)
+
+
+def vshard_task(fa, comm, rank, n, T, V, k, seed):
+    import flexflow_amd.ffmi as F
+    from hip_util import Buf
+    L = F.lib()
+    x = planted_logits(T, V, seed)
+    Vl = V // n
+    shard = Buf(np.ascontiguousarray(x[:, rank * Vl:(rank + 1) * Vl]))
+    ids, probs = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+    scratch = Buf.empty((L.ffmi_vocab_shard_scratch_bytes(n, T),), np.uint8)
+    F.check(L.ffmi_vocab_shard_topk(comm.handle, shard.ptr, T, Vl, k, ids.ptr, probs.ptr,
+                                    scratch.ptr, None), "vocab shard topk")
+    out = {"ids": ids.get(), "probs": probs.get()}
+    if rank == 0:  # the unsharded kernel on the gathered logits
+        full = Buf(x)
+        i1, p1 = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+        if k == 1:
+            F.check(L.ffmi_argmax(full.ptr, T, V, i1.ptr, p1.ptr, None), "argmax")
+        else:
+            F.check(L.ffmi_arg_topk(full.ptr, T, V, k, i1.ptr, p1.ptr, None), "arg_topk")
+        out["ref_ids"], out["ref_probs"] = i1.get(), p1.get()
+    return out

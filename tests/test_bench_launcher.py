@@ -26,6 +26,7 @@ def test_self_launch_spawns_ranks_and_prints_one_line():
     assert len(lines) == 1, p.stdout
     d = json.loads(lines[0])
     assert d["n_gpus"] == 3 and d["max_over_ranks"] == 2.0
+    assert d["allgather"] == ["r0", "r1", "r2"]  # the handle exchange of the xGMI transport
 
 
 def test_dead_rank_fails_fast():

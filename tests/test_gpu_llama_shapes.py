@@ -66,21 +66,28 @@ def test_linear_at_baseline_shapes(shape, T):
         y = unpack_act_np(y.reshape(-1), T, N)
         g = O.linear(X.astype(np.float32), Wg.astype(np.float32))
         u = O.linear(X.astype(np.float32), Wu.astype(np.float32))
-        ref = O.silu_mul(g, u)
-        # a 1-ulp flip of the rounded gate or up value (fp32 reordering at
-        # a rounding boundary) moves the output by ulp(g)*|u*dsilu| or
-        # ulp(u)*|silu(g)|, which can be many output ulps near zero: allow
-        # exactly that, per element
-        sg = 1.0 / (1.0 + np.exp(-g))
-        dsilu = sg * (1.0 + g * (1.0 - sg))
-        ulp = lambda x: np.spacing(np.abs(x).astype(np.float16)).astype(np.float32)  # noqa: E731
-        flip = 1.5 * (ulp(g) * np.abs(u * dsilu) + ulp(u) * np.abs(g * sg))
-        d = np.abs(y.astype(np.float32) - ref)
-        # (+ up to 3 ulp of the output from the chain's own roundings)
-        # (ulp taken at the larger of the two values: they may straddle a binade)
-        excess = d - (flip + 3 * ulp(np.maximum(np.abs(ref), np.abs(y.astype(np.float32)))))
-        assert (excess <= 0).all(), float(excess.max())
-        assert (y.astype(np.float16) == ref.astype(np.float16)).mean() >= 0.99
+        # the epilogue rounds gate and up to fp16, then runs the reference's
+        # half chain (sigmoid_silu_multi.cu:41-46).  With the oracle's gate/up
+        # rounded the same way, >= 99% of the outputs are bit-identical; the
+        # rest must be the chain applied to gate/up values within the plain
+        # GEMMs' tolerance (close16: 2 fp16 ulp or 1e-4 * max |ref|) of the
+        # oracle's -- near zero the fp32 summation order moves gate/up by
+        # several fp16 ulps -- i.e. within [min, max] of the chain over that
+        # box, + 1 output ulp.
+        g16, u16 = g.astype(np.float16), u.astype(np.float16)
+        chain = lambda a, b: O.silu_mul(a.astype(np.float32), b.astype(np.float32))  # noqa: E731
+        ref = chain(g16, u16).astype(np.float16)
+        y16 = y.astype(np.float16)
+        assert (y16 == ref).mean() >= 0.99, (y16 == ref).mean()
+        sp = lambda a: np.spacing(np.abs(a).astype(np.float16)).astype(np.float32)  # noqa: E731
+        dg = np.maximum(2 * sp(g16), 1e-4 * np.abs(g).max())
+        du = np.maximum(2 * sp(u16), 1e-4 * np.abs(u).max())
+        pts = [chain(g + a * dg, u + b * du) for a in (-1, 0, 1) for b in (-1, 0, 1)]
+        lo, hi = np.min(pts, axis=0), np.max(pts, axis=0)
+        yf = y16.astype(np.float32)
+        slack = sp(np.maximum(np.abs(lo), np.abs(hi)))
+        bad = (yf < lo - slack) | (yf > hi + slack)
+        assert not bad.any(), (np.argwhere(bad)[:5], y16[bad][:5], ref[bad][:5])
     else:
         ref = O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1)
         close16(y, ref)

@@ -1,0 +1,94 @@
+"""Direct xGMI all-reduce (kernels/collective.hip) across rank PROCESSES.
+
+The reference all-reduces the row-parallel outputs with ncclAllReduce
+(allreduce_kernels.cu:53-75).  Here the ranks are separate processes that
+exchange through IPC-mapped buffers (tests/peer_group.py); on the one-GPU
+test box they share device 0.  Bar: bit-exact against the rank-order fp32
+sum rounded once (the transport's stated semantics), on every rank, over
+back-to-back rounds that cycle the epochs and buffer parities; a silent peer
+is an error after the timeout, never a hang.
+"""
+import numpy as np
+import pytest
+
+import peer_tasks as PT
+from peer_group import run_group
+
+pytestmark = pytest.mark.gpu
+
+# (count, dtype): one-shot sizes and >= 256 KiB (two-shot for n > 2), and a
+# count that does not split evenly over the ranks' chunks
+CASES = [(8, "f16"), (4096, "f32"), (168 * 4096, "f16"), (8 * 8192 + 24, "f16"),
+         (3 * 65536 + 8, "f32")]
+
+
+@pytest.mark.parametrize("n,two_shot", [(2, False), (2, True), (3, False), (4, False)])
+def test_peer_allreduce_exact(n, two_shot):
+    env = {"FFMI_PEER_TWO_SHOT_MIN": "0"} if two_shot else {}
+    res = run_group(n, PT.ar_task, (CASES, 3), env=env, max_bytes=4 << 20)
+    for it in range(3):
+        for ci, (count, dtype) in enumerate(CASES):
+            want = PT.expected_sum(ci, it, n, count, dtype)
+            for r in range(n):
+                got = res[r][(it, ci)]
+                assert got.dtype == want.dtype
+                np.testing.assert_array_equal(got, want, err_msg=f"rank {r} case {ci} round {it}")
+
+
+def test_peer_allreduce_silent_peer_times_out():
+    res = run_group(2, PT.silent_peer_task, env={"FFMI_PEER_TIMEOUT_S": "1"})
+    r0 = res[0]
+    assert r0["status"] != 0, r0
+    assert "timeout" in r0["msg"], r0
+    assert r0["seconds"] < 30, r0
+
+
+CFG4 = dict(num_layers=2, vocab_size=1000, num_heads=4, num_kv_heads=4, hidden=256,
+            intermediate=512, rms_eps=1e-6, rope_theta=10000.0)
+
+
+@pytest.mark.parametrize("n,T,V,k", [(2, 168, 4096, 1), (4, 37, 32000, 3), (4, 168, 32000, 1),
+                                     (8, 24, 32000, 3)])
+def test_vocab_shard_topk_matches_unsharded(n, T, V, k):
+    """Vocab-parallel lm_head tail (model.cc:3392-3419): every rank's global
+    top-k ids and fp16 probabilities are bit-identical to the unsharded
+    softmax-argmax / top-k kernel, planted cross-shard ties included (lowest
+    index among equal fp16 probabilities)."""
+    res = run_group(n, PT.vshard_task, (T, V, k, 1234 + n), max_bytes=1 << 20)
+    ref_i, ref_p = res[0]["ref_ids"], res[0]["ref_probs"]
+    for r in range(n):
+        np.testing.assert_array_equal(res[r]["ids"], ref_i, err_msg=f"rank {r}")
+        np.testing.assert_array_equal(res[r]["probs"], ref_p, err_msg=f"rank {r}")
+
+
+CFG4V = dict(CFG4, vocab_size=1024)  # V/TP a multiple of 16: lm_head vocab-sharded
+
+
+@pytest.mark.parametrize("tp,overlap,cfg", [(2, "1", CFG4), (2, "0", CFG4), (4, "1", CFG4),
+                                            (2, "1", CFG4V), (4, "1", CFG4V)])
+def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
+    """TP shards as separate processes over the xGMI transport (row-parallel
+    GEMMs in two column halves, each all-reduced on a second stream while the
+    next half computes; the step graphed): every rank emits the same tokens,
+    and they are oracle-valid greedy picks of the UNSHARDED model (ties within
+    2*TP fp16 ulp, as test_gpu_tp_local)."""
+    from test_gpu_e2e import SSM_CFG, check_tokens_vs_oracle, prompts
+    ps = prompts(4, cfg["vocab_size"], 4, 30, 7)
+    res = run_group(tp, PT.model_task, (cfg, 11, ps, 56, False, SSM_CFG),
+                    env={"FFMI_TP_OVERLAP": overlap}, max_bytes=1 << 20)
+    for r in range(1, tp):
+        assert res[r] == res[0]
+    for p, toks in zip(ps, res[0]):
+        assert len(toks) == 56
+        check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp)
+
+
+def test_peer_tp2_spec_infer_equals_incr():
+    """SpecInfer over the transport: identical to incremental decoding of the
+    same sharded model (the reference invariant, cpp_inference_tests.sh:183-189)."""
+    from test_gpu_e2e import SSM_CFG, prompts
+    ps = prompts(3, CFG4V["vocab_size"], 5, 30, 9)
+    ssm = dict(SSM_CFG, vocab_size=1024)
+    inc = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, False, ssm), max_bytes=1 << 20)
+    spec = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, True, ssm), max_bytes=1 << 20)
+    assert spec[0] == spec[1] == inc[0] == inc[1]

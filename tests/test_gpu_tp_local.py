@@ -68,7 +68,8 @@ def run_tp(cfg, seed, tp, ps, max_length, spec=False):
     return out
 
 
-@pytest.mark.parametrize("cfg,tp", [(LLM_CFG, 2), (CFG4, 2), (CFG4, 4), (CFG8, 8)])
+@pytest.mark.parametrize("cfg,tp", [(LLM_CFG, 2), (CFG4, 2), (CFG4, 4), (CFG8, 8),
+                                    (dict(CFG4, vocab_size=1024), 4)])
 def test_tp_shards_decode_like_unsharded_model(cfg, tp):
     ps = prompts(4, cfg["vocab_size"], 4, 30, 7)
     res = run_tp(cfg, 11, tp, ps, 56)
