@@ -403,6 +403,9 @@ def main():
                        tp_rank=rank, tp_size=world, comm=comm, weights_folder=args.llm_weights)
         rm = fa.RequestManager(**rm_kw)
     init_s = time.time() - t_init
+    if os.environ.get("FFMI_DUMP_MAPS"):  # diagnostics: library layout of this process
+        with open("/proc/self/maps") as f, open(os.environ["FFMI_DUMP_MAPS"], "w") as g:
+            g.write(f.read())
 
     for _ in range(args.warmup):
         run_generate(rm, llm, prompts, max_len, spec)

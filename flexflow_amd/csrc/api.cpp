@@ -516,6 +516,7 @@ extern "C" ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *nam
 // mid-step returns an error to the others instead of hanging them).
 struct LocalGroup {
   int n = 0;
+  ffmi_status sum_status = FFMI_OK;  // rank 0's group sum, checked by every rank
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0;
@@ -607,11 +608,13 @@ static ffmi_status local_allreduce(ffmi_comm *c, const void *in, void *out, size
       st = FFMI_ERR_HIP;
     }
   }
-  if (!g.barrier() || st != FFMI_OK) {
+  if (c->rank == 0) g.sum_status = st;  // published by the barrier below
+  if (!g.barrier() || g.sum_status != FFMI_OK) {
+    // rank 0's sum failed (OOM / HIP error): no rank copies g.tmp
     std::lock_guard<std::mutex> lk(g.mu);
     g.broken = true;
     g.cv.notify_all();
-    return st != FFMI_OK ? st : FFMI_ERR_NCCL;
+    return g.sum_status != FFMI_OK ? g.sum_status : FFMI_ERR_NCCL;
   }
   FFMI_HIP(hipMemcpyAsync(out, g.tmp, bytes, hipMemcpyDeviceToDevice, s));
   FFMI_HIP(hipStreamSynchronize(s));

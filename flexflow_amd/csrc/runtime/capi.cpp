@@ -42,14 +42,6 @@ extern "C" ffmi_status ffmi_set_device(int device) {
   return hipSetDevice(device) == hipSuccess ? FFMI_OK : FFMI_ERR_HIP;
 }
 
-extern "C" ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
-                                                   int max_seq, int max_tree, uint64_t salt,
-                                                   int disagree_pct, ffmi_model **out) {
-  if (!out) return FFMI_ERR_INVALID;
-  return ffmi::create_hash_model(vocab, mode, max_requests, max_seq, max_tree, salt,
-                                 disagree_pct, out);
-}
-
 extern "C" ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out) {
   if (!cfg || !out) return FFMI_ERR_INVALID;
   if (cfg->max_requests_per_batch <= 0 ||

@@ -15,6 +15,7 @@
 #include <vector>
 
 #include "model.h"
+#include "../../../include/ffmi_test.h"
 
 namespace ffmi {
 
@@ -120,3 +121,12 @@ ffmi_status create_hash_model(int vocab, int mode, int max_requests, int max_seq
 }
 
 }  // namespace ffmi
+
+// Built into libffmi_testmodel.so (tests only), never into libffmi.so.
+extern "C" ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
+                                                   int max_seq, int max_tree, uint64_t salt,
+                                                   int disagree_pct, ffmi_model **out) {
+  if (!out) return FFMI_ERR_INVALID;
+  return ffmi::create_hash_model(vocab, mode, max_requests, max_seq, max_tree, salt,
+                                 disagree_pct, out);
+}

@@ -362,7 +362,11 @@ struct LlamaGPU : public ffmi_model {
       }
       if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
     }
-    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * 2 * sizeof(int32_t), 0));
+    // coherent (uncached) pinned memory: the sampling kernel's stores go
+    // straight over PCIe and are visible to the host once the stream has
+    // synchronised, whatever HIP_HOST_COHERENT says
+    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * 2 * sizeof(int32_t),
+                           hipHostMallocCoherent | hipHostMallocMapped));
     // weights (seeded synthetic, orc_gen_weight spec), packed for MFMA
     uint16_t *tmp = nullptr;
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));

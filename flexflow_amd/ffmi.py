@@ -171,8 +171,6 @@ SIGNATURES = {
     "ffmi_rm_get_output": (c_int, [c_void_p, c_int64, ctypes.POINTER(c_int), c_int]),
     "ffmi_rm_get_profile": (c_int, [c_void_p, c_int64, ctypes.POINTER(Profile)]),
     "ffmi_rm_get_stats": (c_int, [c_void_p, ctypes.POINTER(ServeStats)]),
-    "ffmi_test_hash_model_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_uint64, c_int,
-                                            ctypes.POINTER(c_void_p)]),
     "ffmi_status_str": (ctypes.c_char_p, [c_int]),
     "ffmi_version": (ctypes.c_char_p, []),
     "ffmi_last_error": (ctypes.c_char_p, []),
@@ -184,7 +182,29 @@ SIGNATURES = {
     "ffmi_debug_attn_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
 }
 
+# test doubles: libffmi_testmodel.so (include/ffmi_test.h), never the product
+TEST_SIGNATURES = {
+    "ffmi_test_hash_model_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_uint64, c_int,
+                                            ctypes.POINTER(c_void_p)]),
+}
+TEST_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libffmi_testmodel.so")
+
 _lib = None
+_test_lib = None
+
+
+def test_lib():
+    """The test-double library (scheduler hash model), loaded after lib()."""
+    global _test_lib
+    if _test_lib is None:
+        lib()
+        L = ctypes.CDLL(TEST_LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in TEST_SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _test_lib = L
+    return _test_lib
 
 
 def lib():

@@ -81,7 +81,7 @@ class HashModel(Model):
                  max_tree_tokens=23, salt=0, disagree_pct=0):
         self.mode = mode
         h = ctypes.c_void_p()
-        F.check(F.lib().ffmi_test_hash_model_create(vocab, self.MODES[mode], max_requests,
+        F.check(F.test_lib().ffmi_test_hash_model_create(vocab, self.MODES[mode], max_requests,
                                                     max_seq_len, max_tree_tokens, salt,
                                                     disagree_pct, ctypes.byref(h)),
                 "hash model")

@@ -410,13 +410,7 @@ typedef struct {
 } ffmi_serve_stats;
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 
-/* Scheduler test double (no GPU): a deterministic hash "model" whose next
- * token is a function of the exact token context each query sees through the
- * KV-slot / bitmask rules, so the RequestManager's batching, tree build,
- * verification and commit lists can be checked on CPU.  TEST USE ONLY. */
-ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
-                                        int max_seq, int max_tree, uint64_t salt,
-                                        int disagree_pct, ffmi_model **out);
+
 
 /* Diagnostics: with FFMI_GEMM_STAMP set in the environment, M-split GEMM
  * launches record per-wave timestamps; copies the last launch's records

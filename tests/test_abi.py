@@ -9,8 +9,8 @@ import flexflow_amd.ffmi as F
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    src = open(os.path.join(ROOT, "include", "ffmi.h")).read()
+def declared_functions(header="ffmi.h"):
+    src = open(os.path.join(ROOT, "include", header)).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(ffmi_[a-z0-9_]+)\s*\(", src)))
 
@@ -21,6 +21,18 @@ def test_header_symbols_exported():
     assert len(names) >= 35
     missing = [n for n in names if not hasattr(lib, n)]
     assert not missing, missing
+
+
+def test_test_doubles_live_outside_the_product_library():
+    """The scheduler hash model (include/ffmi_test.h) is exported by
+    libffmi_testmodel.so only; libffmi.so carries no test symbols."""
+    prod = ctypes.CDLL(F.LIB_PATH)
+    test = ctypes.CDLL(F.TEST_LIB_PATH)
+    names = declared_functions("ffmi_test.h")
+    assert names == ["ffmi_test_hash_model_create"]
+    for n in names:
+        assert hasattr(test, n) and not hasattr(prod, n), n
+    assert set(names) <= set(F.TEST_SIGNATURES)
 
 
 def test_binding_covers_header():

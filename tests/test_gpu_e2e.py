@@ -239,7 +239,11 @@ def test_weight_stream_policy_same_tokens(monkeypatch):
     """FFMI_W_STREAM (non-temporal weight loads; on by default only for
     models larger than the Infinity Cache, so the small test models run
     without it) changes no token: forced on vs forced off, incr decoding
-    and SpecInfer."""
+    and SpecInfer.  These models have K <= 512, where the hint changes no
+    summation order; at long K (>= 8 batches of k-steps per wave, LLaMA-7B
+    o/down at decode) it also selects the 4-wave skinny split, a different
+    fp32 order -- covered within the GEMM tolerance by
+    test_gpu_llama_shapes (W_STREAM at the exact 7B / 65B-TP8 shapes, T = 8)."""
     ps = prompts(4, 1000, 5, 40, 8)
 
     def both():
@@ -252,3 +256,21 @@ def test_weight_stream_policy_same_tokens(monkeypatch):
     monkeypatch.setenv("FFMI_W_STREAM", "0")
     off = both()
     assert on == off
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_result_copy_modes_same_tokens(monkeypatch, graphs):
+    """Sampling results stored by the kernel straight into coherent pinned
+    host memory (default) vs a device buffer + copy (FFMI_RESULT_COPY=1):
+    identical tokens, graphed and eager."""
+    ps = prompts(4, 1000, 5, 40, 12)
+    if not graphs:
+        monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
+    out = []
+    for mode in ("0", "1"):
+        monkeypatch.setenv("FFMI_RESULT_COPY", mode)
+        inc, _ = run_incr(ps, 60)
+        spec, _ = run_spec(ps, 60, SSM_CFG, 5)
+        out.append(([r.output_tokens for r in inc], [r.output_tokens for r in spec]))
+    assert out[0] == out[1]
+    assert out[0][0] == out[0][1]  # and SpecInfer == incremental decoding
