@@ -372,17 +372,19 @@ extern "C" ffmi_status ffmi_linear_pack_weight(const void *W, int out_dim, int i
                                                void *W_packed, ffmi_stream stream) {
   FFMI_CHECK(W && W_packed && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
   FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)W, in_dim, 0, 0, out_dim, in_dim,
-                                    (uint16_t *)W_packed, 0, 0, (hipStream_t)stream));
+                                    (uint16_t *)W_packed, 1, 0, (out_dim + 15) / 16,
+                                    (hipStream_t)stream));
   return FFMI_OK;
 }
 
 extern "C" ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, int out_dim,
                                                 int in_dim, void *W_packed, ffmi_stream stream) {
   FFMI_CHECK(Wg && Wu && W_packed && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
+  const int pitch = 2 * ((out_dim + 15) / 16);
   FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)Wg, in_dim, 0, 0, out_dim, in_dim,
-                                    (uint16_t *)W_packed, 1, 0, (hipStream_t)stream));
+                                    (uint16_t *)W_packed, 2, 0, pitch, (hipStream_t)stream));
   FFMI_HIP(ffmi::launch_pack_weight((const uint16_t *)Wu, in_dim, 0, 0, out_dim, in_dim,
-                                    (uint16_t *)W_packed, 1, 1, (hipStream_t)stream));
+                                    (uint16_t *)W_packed, 2, 1, pitch, (hipStream_t)stream));
   return FFMI_OK;
 }
 

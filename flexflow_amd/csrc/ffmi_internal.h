@@ -115,15 +115,27 @@ __device__ __forceinline__ float partials_value(const float *p, int S, int NP, i
 // ---- kernel launchers (defined in kernels/*.hip) ----
 hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
                               hipStream_t s);
+// Packed weights (weights.hip): 1 KiB block (tile t, k-step kt) at
+// t * w_tile_stride(KT) + kt * w_k_stride(P) halves, P = tiles per k-row of
+// the allocation.  K-major unless FFMI_W_TILE_MAJOR=1 (A/B runs).
+bool weights_kmajor();
+inline size_t w_tile_stride(int KT) { return weights_kmajor() ? 512 : (size_t)KT * 512; }
+inline size_t w_k_stride(int pitch) { return weights_kmajor() ? (size_t)pitch * 512 : 512; }
+// Source rows [row0, row0+N) x columns [col0, col0+K) of a row-major [.][ld]
+// matrix -> destination tiles tile_step * nt + tile_offset of a packed
+// allocation of `pitch` tiles per k-row (gate/up: step 2, offsets 0/1; qkv:
+// offsets 0, NT, 2 NT of pitch 3 NT).
 hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
-                              int N, int K, uint16_t *dst, int interleave_gate_up,
-                              int tile_offset, hipStream_t s);
+                              int N, int K, uint16_t *dst, int tile_step,
+                              int tile_offset, int pitch, hipStream_t s);
 // defer != nullptr: a split-K plan skips its reduce pass and describes the
 // slabs in *defer (the caller's next kernel combines them); otherwise / S == 1
-// Y is written and defer->S = 0.  Only for FFMI_EPI_NONE.
+// Y is written and defer->S = 0.  Only for FFMI_EPI_NONE.  wpitch: tiles per
+// k-row of Wp's allocation (0 = the GEMM's own tile count; a column chunk of a
+// wider matrix passes the full matrix's).
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
-                       Partials *defer = nullptr);
+                       Partials *defer = nullptr, int wpitch = 0);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
 long attn_debug_stamps(long long *dst, long max_waves);
 long gemm_debug_stamps(long long *dst, long max_waves);

@@ -62,7 +62,7 @@ template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false, bool NTL = 
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
-    int NTILES, int xp, int yp) {
+    int NTILES, int xp, int yp, size_t wts, size_t wks) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
@@ -98,7 +98,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 #pragma unroll
   for (int j = 0; j < NT; ++j) {
     int t = min(tile0 + j, NTILES - 1);
-    wrow[j] = Wp + (size_t)t * KT * 512 + lane * 8;
+    wrow[j] = Wp + (size_t)t * wts + lane * 8;
   }
 
   int kt = kb;
@@ -115,7 +115,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         for (int u = 0; u < UP; ++u)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
-            bb[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(k0 + u) * 512);
+            bb[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(k0 + u) * wks);
 #pragma unroll
         for (int u = 0; u < UP; ++u)
 #pragma unroll
@@ -166,7 +166,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(kt + u) * 512);
+        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(kt + u) * wks);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -198,7 +198,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
       const int kk = min(kt + u, ke - 1);
 #pragma unroll
       for (int j = 0; j < NT; ++j)
-        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)kk * 512);
+        b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)kk * wks);
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
@@ -295,7 +295,8 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 template <int MT, int NT, int KW, int U, int EPI>
 static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws, int T,
                       int N, int K, int KT, int NTILES, int S, hipStream_t s, int xp, int yp,
-                      bool nt) {
+                      bool nt, int wpitch) {
+  const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch);
   const int ncb = (NTILES + NT - 1) / NT;
   dim3 grid(ncb, S);
   size_t lds = KW > 1 ? (size_t)(KW - 1) * MT * NT * 4 * 64 * sizeof(float) : 0;
@@ -309,7 +310,7 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
   const bool pipe = force >= 0 ? force != 0 : per_wave >= 2 * U;
 #define FFMI_SKINNY_LAUNCH(PP, NL)                                                             \
   hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, PP, NL>), grid, dim3(KW * 64), lds, \
-                     s, X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp)
+                     s, X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp, wts, wks)
   if (pipe) {
     if (nt) FFMI_SKINNY_LAUNCH(true, true);
     else FFMI_SKINNY_LAUNCH(true, false);
@@ -337,10 +338,11 @@ static int skinny_split(int T, int N, int K, int epi, bool deferrable) {
 template <int MT, int U>
 static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                               int T, int N, int K, int KT, int epi, int S, hipStream_t s,
-                              int xp, int yp, bool nt) {
+                              int xp, int yp, bool nt, int wpitch) {
   int ntiles = (N + 15) / 16;
+  if (!wpitch) wpitch = epi == FFMI_EPI_SILU_MUL ? 2 * ntiles : ntiles;
   if (epi == FFMI_EPI_SILU_MUL)
-    return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt);
+    return run<MT, 2, 4, U, 1>(X, Wp, Y, ws, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt, wpitch);
   // diagnostics: FFMI_SKINNY="NT,KW" forces the tile count and K-split waves
   // of every unsplit skinny launch (A/B runs, scripts/gemm_bench.py)
   static int fnt = -1, fkw = 0;
@@ -349,22 +351,22 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
     if (const char *e = getenv("FFMI_SKINNY")) (void)sscanf(e, "%d,%d", &fnt, &fkw);
   }
   if (fnt > 0 && S == 1 && MT <= 2) {
-    if (fnt == 1 && fkw == 4) return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 1 && fkw == 8) return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 2 && fkw == 4) return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 2 && fkw == 8) return run<MT, 2, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
-    if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt);
+    if (fnt == 1 && fkw == 4) return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 1 && fkw == 8) return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 2 && fkw == 4) return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 2 && fkw == 8) return run<MT, 2, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+    if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
   }
   // wide layers (lm_head): two tiles per workgroup once there are >= 2 row
   // tiles (SSM lm_head at T = 24: 16.1 -> 12.3 us warm; at one row tile a
   // single tile stays faster: LLaMA-7B lm_head T = 8 cold 47.8 vs 55.8 us)
   if (MT >= 2 && ntiles >= 512)
-    return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
+    return run<MT, 2, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt, wpitch);
   // 8-wave groups only where the accumulators fit 2 waves/SIMD (no spills)
   if (ntiles >= 512 || MT >= 8)
-    return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
+    return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt, wpitch);
   // ... and where each wave still gets a full batch of U k-steps (K = 768 of
   // the SSM: 4 waves x 6 k-steps beat 8 x 3, qkv T = 24: 5.7 -> 4.2 us).
   // Non-temporal weight loads (FFMI_W_STREAM) keep 4 waves at every row-tile
@@ -374,8 +376,8 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
   // policy) only, not on T: the threshold is a fixed 64 k-steps per slice
   // (8 waves x the largest batch U = 8), never U itself, which depends on T.
   if ((KT + S - 1) / S >= 64 && !nt)
-    return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
-  return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt);
+    return run<MT, 1, 8, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt, wpitch);
+  return run<MT, 1, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, S, s, xp, yp, nt, wpitch);
 }
 
 // ---------------------------------------------------------------------------
@@ -459,7 +461,7 @@ template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false
 __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
-    int NTILES, int S, int yp) {
+    int NTILES, int S, int yp, size_t wts, size_t wks) {
   long long st0 = 0, st1 = 0, st2 = 0;
   if (STAMP) st0 = rt_now();
   static_assert(NTW % 2 == 0, "gate/up tiles come in pairs");
@@ -487,7 +489,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     // per k-step: loads behind a wave-dependent branch are invisible to the
     // compiler's vmcnt counting, which then waits for ~2 ring slots, not PF-1
     const int t = min(tile0 + (ULD ? min(bj[p], NTW - 1) : bj[p]), NTILES - 1);
-    bsrc[p] = Wp + (size_t)t * KT * 512 + lane * 8;
+    bsrc[p] = Wp + (size_t)t * wts + lane * 8;
   }
   // X row-major [T][K] (16 rows x 64 B per fragment load), or XP: packed
   // activation tiles [T/16][KT][64 lanes][8] (one contiguous 1 KiB per load)
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kq * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kq * wks);
     }
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
@@ -551,7 +553,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
       for (int i = 0; i < NV; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * XS);
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
-        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kw * 512);
+        if (ULD || NTW % 4 == 0 || bj[p] < NTW) bq[Q][p] = ld_weight<NTL>(bsrc[p] + (size_t)kw * wks);
       // B(kt+1) lives in ring slot (Q+1) % PF
 #pragma unroll
       for (int p = 0; p < PPT; ++p)
@@ -722,9 +724,10 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
 template <int MTW, int NTW, int PF>
 static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s,
-                          bool xpacked, int yp, int S, Partials *defer, bool nt) {
+                          bool xpacked, int yp, int S, Partials *defer, bool nt, int wpitch) {
   const int KT = K / 32;
   const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
+  const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch ? wpitch : ntiles);
   const int mtiles = (T + 15) / 16;
   const int mblocks = (mtiles + 4 * MTW - 1) / (4 * MTW);
   const int nblk = (ntiles + NTW - 1) / NTW;
@@ -741,7 +744,7 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   const bool ntl = nt && mblocks == 1;
 #define FFMI_MID2(E, ST, XPK, U, NL)                                                               \
   hipLaunchKernelGGL((gemm_mid_kernel<MTW, NTW, PF, E, ST, XPK, U, NL>), grid, dim3(256), 0, s, X, \
-                     Wp, Y, ws, T, N, K, KT, ntiles, S, yp)
+                     Wp, Y, ws, T, N, K, KT, ntiles, S, yp, wts, wks)
 #define FFMI_MID(E, ST, XPK)                                  \
   do {                                                        \
     const bool u_ = uld && NTW % 4;                           \
@@ -793,7 +796,7 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
 
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
-                       Partials *defer) {
+                       Partials *defer, int wpitch) {
   if (defer) defer->S = 0;
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
@@ -806,7 +809,8 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   if (mtiles > 4) {
     const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);
 #define FFMI_RUN(M, NW) \
-  return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer, nt)
+  return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer, nt, \
+                           wpitch)
     if (p.MTW == 3) {
       if (p.NTW == 2) FFMI_RUN(3, 2);
       if (p.NTW == 4) FFMI_RUN(3, 4);
@@ -828,9 +832,9 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   const size_t need = (size_t)S * T * ((N + 15) / 16) * 16 * sizeof(float);
   if (S > 1 && (!ws || ws_bytes < need)) S = 1;
   hipError_t e;
-  if (mtiles <= 1) e = dispatch_nt<1, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
-  else if (mtiles <= 2) e = dispatch_nt<2, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
-  else e = dispatch_nt<4, 4>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt);
+  if (mtiles <= 1) e = dispatch_nt<1, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt, wpitch);
+  else if (mtiles <= 2) e = dispatch_nt<2, 8>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt, wpitch);
+  else e = dispatch_nt<4, 4>(X, Wp, Y, ws, T, N, K, KT, epilogue, S, s, xi, yp, nt, wpitch);
   if (S > 1 && e == hipSuccess) defer->p = ws, defer->S = S, defer->NP = (N + 15) / 16 * 16;
   return e;
 }

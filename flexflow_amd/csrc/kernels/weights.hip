@@ -6,11 +6,16 @@
 // weights without shipping checkpoints (none exist offline).
 //
 // Packed layout ("MFMA B-fragment order") for Y = X . W^T with
-// v_mfma_f32_16x16x32_f16: the [N][K] matrix is cut into 16x32 blocks; block
-// (nt, kt) is 1 KiB at ((nt * KT) + kt) * 512 halves, and lane l of a wave
-// owns halves [l*8, l*8+8) = W[nt*16 + (l&15)][kt*32 + 8*(l>>4) + 0..7],
-// exactly the B operand the MFMA wants.  A wave streaming one N-tile reads
-// contiguous 1 KiB per k-step (fully coalesced, 16 B/lane).
+// v_mfma_f32_16x16x32_f16: the [N][K] matrix is cut into 16x32 blocks, 1 KiB
+// each; lane l of a wave owns halves [l*8, l*8+8) = W[nt*16 + (l&15)][kt*32 +
+// 8*(l>>4) + 0..7], exactly the B operand the MFMA wants, so a wave streaming
+// one N-tile reads contiguous 1 KiB per k-step (fully coalesced, 16 B/lane).
+// Blocks are stored K-MAJOR: block (nt, kt) at (kt * P + nt) * 512 halves,
+// P = the allocation's tiles per k-row (w_tile_stride / w_k_stride).  All
+// workgroups of a GEMM walk k in step, so at any moment the chip reads one
+// contiguous band of k-row kt instead of ~230 streams 128 KiB apart: the
+// T = 168 gate/up loop went 57 -> 44 us in scripts/probe/xl2_probe.hip (the
+// old tile-major order, FFMI_W_TILE_MAJOR=1, stays for A/B runs).
 #include "../ffmi_internal.h"
 
 namespace ffmi {
@@ -56,8 +61,8 @@ uint64_t weight_key(const char *name, uint64_t seed) {
 // One thread per (block, lane): gathers 8 halves of W[row][k..k+7].
 __global__ void pack_weight_kernel(const uint16_t *__restrict__ src, int ld, int row0,
                                    int col0, int N, int K, int NT, int KT,
-                                   uint16_t *__restrict__ dst, int interleave,
-                                   int tile_offset) {
+                                   uint16_t *__restrict__ dst, int tile_step,
+                                   int tile_offset, size_t ts, size_t ks) {
   long gid = blockIdx.x * (long)blockDim.x + threadIdx.x;
   long total = (long)NT * KT * 64;
   if (gid >= total) return;
@@ -71,23 +76,29 @@ __global__ void pack_weight_kernel(const uint16_t *__restrict__ src, int ld, int
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     v[j] = (n < N && k + j < K) ? src[(size_t)(row0 + n) * ld + col0 + k + j] : 0;
-  long dtile = interleave ? (2L * nt + tile_offset) : nt;
+  const long dtile = (long)tile_step * nt + tile_offset;
   uint4 pk;
   pk.x = v[0] | ((uint32_t)v[1] << 16);
   pk.y = v[2] | ((uint32_t)v[3] << 16);
   pk.z = v[4] | ((uint32_t)v[5] << 16);
   pk.w = v[6] | ((uint32_t)v[7] << 16);
-  *reinterpret_cast<uint4 *>(dst + ((dtile * KT + kt) * 512 + lane * 8)) = pk;
+  *reinterpret_cast<uint4 *>(dst + dtile * ts + kt * ks + lane * 8) = pk;
+}
+
+bool weights_kmajor() {
+  static const bool km = !(getenv("FFMI_W_TILE_MAJOR") && atoi(getenv("FFMI_W_TILE_MAJOR")) != 0);
+  return km;
 }
 
 hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0, int N,
-                              int K, uint16_t *dst, int interleave, int tile_offset,
+                              int K, uint16_t *dst, int tile_step, int tile_offset, int pitch,
                               hipStream_t s) {
   int NT = (N + 15) / 16, KT = (K + 31) / 32;
+  const size_t ts = w_tile_stride(KT), ks = w_k_stride(pitch);
   long total = (long)NT * KT * 64;
   unsigned blocks = (unsigned)((total + 255) / 256);
   hipLaunchKernelGGL(pack_weight_kernel, dim3(blocks), dim3(256), 0, s, src, ld, row0,
-                     col0, N, K, NT, KT, dst, interleave, tile_offset);
+                     col0, N, K, NT, KT, dst, tile_step, tile_offset, ts, ks);
   return hipGetLastError();
 }
 

@@ -382,7 +382,8 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&lm, ffmi_linear_packed_bytes(Vl, H) / 2));
     TRY(fill(tmp, (size_t)V * H, "lm_head.weight", 0));
     // vocab shard s: rows [s*Vl, (s+1)*Vl) (the whole table when replicated)
-    FFMI_HIP(launch_pack_weight(tmp, H, Vl == V ? 0 : o.tp_rank * Vl, 0, Vl, H, lm, 0, 0, stream));
+    FFMI_HIP(launch_pack_weight(tmp, H, Vl == V ? 0 : o.tp_rank * Vl, 0, Vl, H, lm, 1, 0,
+                                (Vl + 15) / 16, stream));
     slots = 0;
     layers.resize(c.num_layers);
     const int s = o.tp_rank;
@@ -400,23 +401,26 @@ struct LlamaGPU : public ffmi_model {
                               "self_attn.v_proj.weight"};
       for (int q = 0; q < 3; ++q) {
         TRY(fill(tmp, (size_t)H * H, p + names[q], 0));
-        FFMI_HIP(launch_pack_weight(tmp, H, s * Hl, 0, Hl, H, L.wqkv + q * qkv_tiles_bytes / 2, 0,
-                                    0, stream));
+        // one allocation of 3 NT tiles per k-row: Q, K, V tiles side by side
+        FFMI_HIP(launch_pack_weight(tmp, H, s * Hl, 0, Hl, H, L.wqkv, 1, q * (Hl / 16),
+                                    3 * (Hl / 16), stream));
       }
       // o_proj: row-parallel -> columns [s*Hl, (s+1)*Hl)
       TRY(alloc(&L.wo, ffmi_linear_packed_bytes(H, Hl) / 2));
       TRY(fill(tmp, (size_t)H * H, p + "self_attn.o_proj.weight", 0));
-      FFMI_HIP(launch_pack_weight(tmp, H, 0, s * Hl, H, Hl, L.wo, 0, 0, stream));
+      FFMI_HIP(launch_pack_weight(tmp, H, 0, s * Hl, H, Hl, L.wo, 1, 0, H / 16, stream));
       // gate | up: column-parallel, interleaved 16-column tiles
       TRY(alloc(&L.wgu, 2 * ffmi_linear_packed_bytes(Fl, H) / 2));
       TRY(fill(tmp, (size_t)F * H, p + "mlp.gate_proj.weight", 0));
-      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 1, 0, stream));
+      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 2, 0, 2 * ((Fl + 15) / 16),
+                                  stream));
       TRY(fill(tmp, (size_t)F * H, p + "mlp.up_proj.weight", 0));
-      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 1, 1, stream));
+      FFMI_HIP(launch_pack_weight(tmp, H, s * Fl, 0, Fl, H, L.wgu, 2, 1, 2 * ((Fl + 15) / 16),
+                                  stream));
       // down: row-parallel -> columns [s*Fl, (s+1)*Fl) of [H][F]
       TRY(alloc(&L.wd, ffmi_linear_packed_bytes(H, Fl) / 2));
       TRY(fill(tmp, (size_t)H * F, p + "mlp.down_proj.weight", 0));
-      FFMI_HIP(launch_pack_weight(tmp, F, 0, s * Fl, H, Fl, L.wd, 0, 0, stream));
+      FFMI_HIP(launch_pack_weight(tmp, F, 0, s * Fl, H, Fl, L.wd, 1, 0, H / 16, stream));
       ffmi_attn_cfg ac;
       ac.mode = mode == FFMI_MODEL_TREE ? FFMI_ATTN_TREE
                                         : (mode == FFMI_MODEL_BEAM ? FFMI_ATTN_SPEC : FFMI_ATTN_INC);
@@ -469,11 +473,12 @@ struct LlamaGPU : public ffmi_model {
       return allreduce(out, (size_t)T * H);
     }
     const int Hc = H / tp_chunks;
-    const size_t tiles = (size_t)(Hc / 16) * ((K + 31) / 32) * 512;  // packed rows of a chunk
+    // a chunk = Hc / 16 consecutive tiles of the H / 16 per k-row
+    const size_t tiles = (size_t)(Hc / 16) * ffmi::w_tile_stride((K + 31) / 32);
     for (int ch = 0; ch < tp_chunks; ++ch) {
       uint16_t *cb = chunk_buf + (size_t)ch * T * Hc;
       FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb, ws, ws_bytes, T, Hc, K, XP, stream,
-                                 nullptr));
+                                 nullptr, H / 16));
       FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
       FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
       ffmi_status st =

@@ -21,6 +21,8 @@ SHAPES = {
                 ("down", 4096, 11008, 0), ("lm_head", 32000, 4096, 0)],
     "ssm": [("qkv", 2304, 768, 0), ("o", 768, 768, 0), ("gate_up", 3072, 768, 1),
             ("down", 768, 3072, 0), ("lm_head", 32000, 768, 0)],
+    # gate/up without its SiLU epilogue (epilogue-cost A/B)
+    "gate_up_plain": [("gate_up_plain", 22016, 4096, 0)],
 }
 
 
@@ -33,6 +35,8 @@ def main():
     ap.add_argument("--wstream", action="store_true",
                     help="non-temporal weight loads (FFMI_W_STREAM, as the LLaMA-7B model)")
     ap.add_argument("--ops", default="", help="comma list of op names to run (default all)")
+    ap.add_argument("--same-x", action="store_true",
+                    help="one activation buffer for every weight copy (L2-warm X)")
     ap.add_argument("--cold-mb", type=int, default=768,
                     help="rotate weight copies totalling this many MB (0: one hot copy)")
     args = ap.parse_args()
@@ -62,7 +66,7 @@ def main():
             assert hip().hipMemcpy(c.ptr, Wp.ptr, nb, 3) == 0
             Wps.append(c)
         for T in [int(t) for t in args.T.split(",")]:
-            Xs = [Buf(f16(rng.standard_normal((T, K)))) for _ in range(len(Wps))]
+            Xs = [Buf(f16(rng.standard_normal((T, K)))) for _ in range(1 if args.same_x else len(Wps))]
             flag = 0
             if args.xpacked and T > 64:
                 flag = F.X_PACKED
@@ -76,12 +80,12 @@ def main():
                 flag |= F.W_STREAM
             Y = Buf.empty((T, N), np.float16)
             for i in range(len(Wps)):
-                F.check(L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None))
+                F.check(L.ffmi_linear(Xs[i % len(Xs)].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None))
             tm = Timer()
             tm.start()
             for it in range(args.iters):
                 i = it % len(Wps)
-                L.ffmi_linear(Xs[i].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None)
+                L.ffmi_linear(Xs[i % len(Xs)].ptr, Wps[i].ptr, Y.ptr, T, N, K, epi | flag, None)
             ms = tm.stop() / args.iters
             byts = 2.0 * (rows * K + T * K + T * N)
             r = dict(op=name, T=T, N=N, K=K, copies=len(Wps), us=round(ms * 1e3, 2),
