@@ -104,18 +104,50 @@ ffmi_status batch_stage(ffmi_batch_dev *b, const ffmi_batch_desc *d, size_t *byt
     // lowest slot this step writes for each item's request (its stores and
     // the TREE commits): the attention kernel may load keys below it before
     // its own KV-update prologue has run
+    // The fused attention stages every slot the step writes for the item's
+    // request in an LDS tail [tail0, tail0 + kTailSlots) and takes the
+    // request's commits from the work item (lds_tail: all items fit)
     ffmi::WorkDev *wd = reinterpret_cast<ffmi::WorkDev *>(b->host + off);
+    b->lds_tail = true;
     for (int wi = 0; wi < d->num_work; ++wi) {
       ffmi::WorkDev x{};
       x.w = d->work[wi];
-      int clean = INT32_MAX;
+      int clean = INT32_MAX, hi = -1;
       for (int t = 0; t < d->num_tokens; ++t)
-        if (d->tokens[t].req == x.w.req && d->tokens[t].store_slot >= 0)
+        if (d->tokens[t].req == x.w.req && d->tokens[t].store_slot >= 0) {
           clean = std::min(clean, (int)d->tokens[t].store_slot);
+          hi = std::max(hi, (int)d->tokens[t].store_slot);
+        }
       for (int c = 0; c < d->num_commits; ++c)
-        if (d->commits[c].req == x.w.req && d->commits[c].depth >= 0)
+        if (d->commits[c].req == x.w.req && d->commits[c].depth >= 0) {
           clean = std::min(clean, (int)d->commits[c].depth);
+          hi = std::max(hi, (int)d->commits[c].depth);
+          if (x.ncommit < ffmi::kItemCommits && d->commits[c].src_token <= 32767 &&
+              d->commits[c].depth <= 32767) {
+            x.cm_src[x.ncommit] = (int16_t)d->commits[c].src_token;
+            x.cm_depth[x.ncommit] = (int16_t)d->commits[c].depth;
+          } else {
+            b->lds_tail = false;
+          }
+          ++x.ncommit;
+        }
       x.clean = clean;
+      x.tail0 = (std::min(clean, (int)x.w.kv_len) / 32) * 32;
+      x.told = std::min(clean, (int)x.w.kv_len) - x.tail0;
+      const int end = std::max(hi + 1, (int)x.w.kv_len);
+      if (end - x.tail0 > ffmi::kTailSlots) {
+        b->lds_tail = false;
+      } else if (clean < end) {  // every slot in [clean, end) written this step
+        bool dense[ffmi::kTailSlots] = {};
+        for (int t = 0; t < d->num_tokens; ++t)
+          if (d->tokens[t].req == x.w.req && d->tokens[t].store_slot >= clean)
+            dense[d->tokens[t].store_slot - clean] = true;
+        for (int c = 0; c < d->num_commits; ++c)
+          if (d->commits[c].req == x.w.req && d->commits[c].depth >= clean)
+            dense[d->commits[c].depth - clean] = true;
+        for (int sl = clean; sl < end; ++sl)
+          if (!dense[sl - clean]) b->lds_tail = false;
+      }
       for (int j = 0; j < FFMI_ATTN_QTILE; ++j) {
         const int t = x.w.q_start + std::min(j, std::max(x.w.q_count - 1, 0));
         const int pos = t < d->num_tokens ? d->tokens[t].pos : 0;
@@ -319,7 +351,7 @@ ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
   // commit-then-store order).  FFMI_ATTN_NO_FUSE=1 forces the two-launch path
   // (A/B and parity tests).
   const bool no_fuse = getenv("FFMI_ATTN_NO_FUSE") != nullptr;
-  const bool fused = b->one_item_per_req && !no_fuse;
+  const bool fused = b->one_item_per_req && b->lds_tail && !no_fuse;
   if (C > 0 && b->commit_overlap) {
     FFMI_HIP(ffmi::launch_commit(b->dev, C, stage_rd, h->kc, h->vc, heads, d, h->slots, s));
     C = 0;

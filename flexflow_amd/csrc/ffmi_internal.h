@@ -65,16 +65,29 @@ struct BatchHeader {
 constexpr int kBlobWorkOffset = 32;
 static_assert(sizeof(BatchHeader) == kBlobWorkOffset, "work array follows the header");
 
+// Fused attention's LDS tail: the keys [tail0, kv_len) of a work item are
+// staged in LDS, at most kTailSlots of them: the slots below the request's
+// lowest written slot (< 32, chunk alignment) from the cache, every slot from
+// there on written this step (its stores and TREE commits, host-checked).  At
+// most kItemCommits commits per request are applied by the attention prologue.
+constexpr int kTailSlots = 128;
+constexpr int kItemCommits = 8;
+
 // Device work item: the ABI item plus what the host derives for the kernels.
 struct WorkDev {
   ffmi_attn_work w;
   int32_t clean;  // slots below this are not written by this step's commits
                   // or stores for the item's request (loadable before them)
-  int32_t pad[3];
+  int32_t tail0;  // chunk-aligned first slot of the LDS tail (<= clean)
+  int32_t ncommit;  // TREE commits of this request (cm_src / cm_depth)
+  int32_t told;     // slots [tail0, tail0 + told) keep their cached K/V (< 32);
+                    // every tail slot above them is written this step
   // RoPE position of each of the item's tokens (clamped to [0, 32767]; the
   // kernels clamp to their table): the table loads then depend on the work
   // item only, not on the token records
   int16_t rope_pos[FFMI_ATTN_QTILE];
+  // the request's commits: staging row (previous verify batch) -> KV slot
+  int16_t cm_src[kItemCommits], cm_depth[kItemCommits];
 };
 static_assert(sizeof(WorkDev) % 16 == 0, "16-B aligned work items");
 
@@ -185,6 +198,8 @@ struct ffmi_batch_dev {
   int num_tokens = 0, num_work = 0, num_commits = 0, num_mask_reqs = 0;
   bool commit_overlap = false;  // a commit depth is also a slot this step stores
   bool one_item_per_req = false;  // every request's tokens form one attention work item
+  bool lds_tail = false;  // every item's writes fit the fused kernel's LDS tail and
+                          // its commits the work item (else the two-launch path)
   int max_q = 0;                  // largest work item
   hipEvent_t uploaded = nullptr;  // guards reuse of the pinned staging
 };

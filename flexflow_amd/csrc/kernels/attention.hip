@@ -94,13 +94,20 @@ __device__ __forceinline__ void st_h4(uint16_t *p, uint16_t a, uint16_t b, uint1
 // after_loads() runs once this thread's update loads are in flight (the
 // fused attention issues its first K/V chunk there: loads complete in issue
 // order, so anything issued BEFORE these would delay them).
-template <int D, int NQ, int NT, class AfterLoads>
+// Tail mode (sKt != nullptr, the fused attention): K rows and V^T columns of
+// the stored tokens also go to the workgroup's LDS tail tile (slot - tail0),
+// where its attention reads them -- no wait for the global stores; V^T then
+// goes to HBM from sVt.  before_stores() runs (in every thread) once the
+// loads are back, before the first store.
+template <int D, int NQ, int NT, class AfterLoads, class BeforeStores>
 __device__ __forceinline__ void kv_update_item(
     const BatchView &bv, const WorkDev *__restrict__ wdp, int h, int heads, int slots, int T,
     const uint16_t *__restrict__ qkv, const float *__restrict__ part, int pS, int pNP,
     const float *__restrict__ rope, int max_rope_pos, uint16_t *__restrict__ qbuf,
     uint16_t *__restrict__ kc, uint16_t *__restrict__ stage_wr, uint16_t (*sV)[NQ + 1],
-    int *sSlot, uint16_t (*sQ)[D + 8], AfterLoads &&after_loads) {
+    int *sSlot, uint16_t (*sQ)[D + 8], uint16_t (*sKt)[D + 8],
+    uint16_t (*sVt)[kTailSlots + 8], int tail0, AfterLoads &&after_loads,
+    BeforeStores &&before_stores) {
   constexpr int HD = D / 2, G = HD / 4, UNITS = NQ * G, U = (UNITS + NT - 1) / NT;
   const int Hl = heads * D;
   const ffmi_attn_work w = wdp->w;
@@ -196,6 +203,7 @@ __device__ __forceinline__ void kv_update_item(
       for (int c = 0; c < 6; ++c) x[u][c] = round_h4(x[u][c]);
   }
 
+  before_stores();
   // ---- stores
 #pragma unroll
   for (int u = 0; u < U; ++u) {
@@ -224,10 +232,23 @@ __device__ __forceinline__ void kv_update_item(
       st_h4(kr + HD, khi[0], khi[1], khi[2], khi[3]);
     }
     if (i0[u] == 0) sSlot[tl[u]] = store ? tslot[u] : -1;
+    if (sKt) {  // (host-checked: every stored slot lies in the tail)
+      if (store) {
+        const int ts = tslot[u] - tail0;
+        st_h4(&sKt[ts][i0[u]], klo[0], klo[1], klo[2], klo[3]);
+        st_h4(&sKt[ts][i0[u] + HD], khi[0], khi[1], khi[2], khi[3]);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      sV[i0[u] + j][tl[u]] = vlo[j];
-      sV[i0[u] + HD + j][tl[u]] = vhi[j];
+        for (int j = 0; j < 4; ++j) {
+          sVt[i0[u] + j][ts] = vlo[j];
+          sVt[i0[u] + HD + j][ts] = vhi[j];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        sV[i0[u] + j][tl[u]] = vlo[j];
+        sV[i0[u] + HD + j][tl[u]] = vhi[j];
+      }
     }
     if (stage_wr) {
       uint16_t *st = stage_wr + (size_t)t * 2 * Hl + h * D + i0[u];
@@ -289,8 +310,9 @@ __global__ __launch_bounds__(FFMI_ATTN_QTILE * D / 8) void kv_update_kernel(
     return;
   }
   const ffmi_attn_work w = bv.work[item].w;
-  kv_update_item<D, NQ, NT>(bv, &bv.work[item], h, heads, slots, T, qkv, part, pS, pNP, rope, max_rope_pos,
-                            qbuf, kc, stage_wr, sV, sSlot, nullptr, [] {});
+  kv_update_item<D, NQ, NT>(bv, &bv.work[item], h, heads, slots, T, qkv, part, pS, pNP, rope,
+                            max_rope_pos, qbuf, kc, stage_wr, sV, sSlot, nullptr, nullptr, nullptr,
+                            0, [] {}, [] {});
   __syncthreads();
   kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
 }
@@ -354,9 +376,18 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   constexpr int KS = D / 32;  // k-steps of the QK^T product
   constexpr int DT = D / 16;  // d-tiles of the PV product
   constexpr int NQ = 16 * QT;
+  constexpr int TS = kTailSlots;
   __shared__ float sm_m[NW][NQ];
   __shared__ float sm_l[NW][NQ];
-  __shared__ __attribute__((aligned(16))) float sm_o[NW][QT][DT][4][64];
+  // the merge buffer shares its LDS with the FUSED tail tile (K rows and V^T
+  // columns of slots [tail0, tail0 + TS)); a barrier separates their uses
+  constexpr int SMO_BYTES = NW * QT * DT * 4 * 64 * 4;
+  constexpr int TAIL_BYTES = FUSED ? (TS * (D + 8) + D * (TS + 8)) * 2 : 0;
+  __shared__ __attribute__((aligned(16)))
+  char smem[SMO_BYTES > TAIL_BYTES ? SMO_BYTES : TAIL_BYTES];
+  auto sm_o = reinterpret_cast<float(*)[QT][DT][4][64]>(smem);
+  auto sKt = reinterpret_cast<uint16_t(*)[D + 8]>(smem);
+  auto sVt = reinterpret_cast<uint16_t(*)[TS + 8]>(smem + TS * (D + 8) * 2);
 
   // ST: lane 0 of each wave stores its timeline straight to kv.stamps
   long long *stp = nullptr;
@@ -375,7 +406,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   // (fields, not a copy of the WorkDev: a private copy of its rope_pos array
   // would be indexed per lane and live in scratch)
   const ffmi_attn_work w = bv.work[blockIdx.x].w;
-  const int clean = bv.work[blockIdx.x].clean;
   const int Hl = heads * D;
   const uint16_t *kbase = kc + ((size_t)w.req * heads + h) * slots * D;
   const uint16_t *vbase = vc + ((size_t)w.req * heads + h) * D * slots;
@@ -397,57 +427,129 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       va[t] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
     }
   };
-  // FUSED: a wave's first chunk lies below every slot this step writes for
-  // the request (host-computed `clean`): its loads go out right after the
-  // KV-update prologue's own loads (kv_update_item's after_loads hook) and
-  // land while the prologue computes and stores.  Only clean chunks of busy
-  // waves are prefetched: issuing every wave's first chunk unconditionally
-  // measured slower in the model (duplicate chunks for idle waves and unclean
-  // chunks cost more port bytes than the in-order wait saves).
+  // FUSED: every slot this step writes for the request (its stores and TREE
+  // commits) lies in the LDS tail [tail0, kv_len) (host-checked, lds_tail);
+  // the keys below tail0 are untouched this step, so their chunks load from
+  // HBM at any time and a wave's first one goes out with the prologue's
+  // loads.  The tail's chunks are read from LDS: the prologue writes the new
+  // K/V there as well as to HBM, and the attention never waits for its own
+  // global stores.
   const int nchunks = (w.kv_len + 31) >> 5;
+  const int tail0 = FUSED ? bv.work[blockIdx.x].tail0 : w.kv_len;
+  const int ctail = tail0 >> 5;  // first chunk read from the LDS tail
   h8 kf0[2][KS], va0[DT];
-  const bool early = FUSED && wave < nchunks && (wave + 1) * 32 <= clean;
+  const bool early = FUSED && wave < nchunks && wave < ctail;
 
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
   __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
   if (FUSED) {
-    __shared__ uint16_t sV[D][NQ + 1];
     __shared__ int sSlot[NQ];
-    // (1) commits of this request (the host launches them separately when a
-    // commit depth coincides with a slot stored below), 16-B rows
+    const WorkDev *wdp = &bv.work[blockIdx.x];
+    constexpr int NT = 64 * NW;
     constexpr int D8 = D / 8;
-    for (int e = threadIdx.x; e < kv.C * D8; e += blockDim.x) {
-      const ffmi_commit_info cm = bv.commits[e / D8];
-      const int i = (e % D8) * 8;
-      if (cm.req != w.req || cm.depth < 0 || cm.depth >= slots) continue;
-      const uint16_t *st = kv.stage_rd + (size_t)cm.src_token * 2 * Hl + h * D + i;
-      const uint4 kk = *reinterpret_cast<const uint4 *>(st);
-      const uint4 vv = *reinterpret_cast<const uint4 *>(st + Hl);
-      *reinterpret_cast<uint4 *>(kc + (((size_t)cm.req * heads + h) * slots + cm.depth) * D + i) = kk;
-      uint16_t *vt = vc + (((size_t)cm.req * heads + h) * D + i) * slots + cm.depth;
-      const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+    // cached contents of the tail's first `told` (< 32) slots, which this
+    // step does not write, 16-B pieces: K rows, then V^T row segments (the
+    // V^T pieces cover the whole first chunk; the written slots among them
+    // are overwritten in LDS after the barrier below)
+    constexpr int TK = (32 * D8 + NT - 1) / NT, TV = (D * 4 + NT - 1) / NT;
+    const int told = bv.work[blockIdx.x].told;
+    uint4 tk[TK], tv[TV];
+    // the request's commits (16-B pieces of the staging K and V rows)
+    constexpr int CP = (kItemCommits * 2 * D8 + NT - 1) / NT;
+    const int ncm = kv.C > 0 ? wdp->ncommit : 0;
+    uint4 cmv[CP];
+    kv_update_item<D, NQ, NT>(
+        bv, wdp, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
+        qbuf, kc, kv.stage_wr, nullptr, sSlot, sQ, sKt, sVt, tail0,
+        [&] {  // after the KV update's own loads: commits, tail, first chunk
 #pragma unroll
-      for (int j = 0; j < 8; ++j) vt[(size_t)j * slots] = (uint16_t)(vw[j >> 1] >> (16 * (j & 1)));
-    }
-    stamp(6);
-    // (2) RoPE + KV store + staging of this item's tokens, this head
-    kv_update_item<D, NQ, 64 * NW>(
-        bv, &bv.work[blockIdx.x], h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
-        qbuf, kc, kv.stage_wr, sV, sSlot, sQ, [&] {
-          // the first clean chunk goes out once the prologue's own loads are
-          // in flight (issued earlier, every prologue wait -- the commit
-          // records, the token records -- also waited for these 24 loads)
+          for (int i = 0; i < CP; ++i) {
+            const int e = threadIdx.x + i * NT, j = e / (2 * D8), r = e % (2 * D8);
+            if (j < ncm) {
+              const int src = wdp->cm_src[j];
+              cmv[i] = *reinterpret_cast<const uint4 *>(
+                  kv.stage_rd + (size_t)src * 2 * Hl + (r >= D8 ? Hl : 0) + h * D + (r % D8) * 8);
+            }
+          }
+#pragma unroll
+          for (int i = 0; i < TK; ++i) {
+            const int e = threadIdx.x + i * NT, row = e / D8;
+            if (row < told)
+              tk[i] = *reinterpret_cast<const uint4 *>(kbase + (size_t)(tail0 + row) * D + (e % D8) * 8);
+          }
+#pragma unroll
+          for (int i = 0; i < TV; ++i) {
+            const int e = threadIdx.x + i * NT, dd = e / 4, s8 = (e % 4) * 8;
+            if (dd < D && s8 < told)
+              tv[i] = *reinterpret_cast<const uint4 *>(vbase + (size_t)dd * slots + tail0 + s8);
+          }
+          // (issued last: the waits below for the loads above leave it in flight)
           if (early) load_chunk(wave, kf0, va0);
+        },
+        [&] {  // loads are back: the old tail to LDS, then the commits
+#pragma unroll
+          for (int i = 0; i < TK; ++i) {
+            const int e = threadIdx.x + i * NT, row = e / D8;
+            if (row < told) *reinterpret_cast<uint4 *>(&sKt[row][(e % D8) * 8]) = tk[i];
+          }
+#pragma unroll
+          for (int i = 0; i < TV; ++i) {
+            const int e = threadIdx.x + i * NT, dd = e / 4, s8 = (e % 4) * 8;
+            if (dd < D && s8 < told) {
+              uint2 *dst = reinterpret_cast<uint2 *>(&sVt[dd][s8]);  // rows are 8-B aligned
+              dst[0] = make_uint2(tv[i].x, tv[i].y);
+              dst[1] = make_uint2(tv[i].z, tv[i].w);
+            }
+          }
+          // keys past kv_len in the last chunk are masked, but P.V still
+          // multiplies their V by 0: zero them (as the cache's never-written
+          // slots are); a stored slot among them is written after the barrier
+          for (int e = threadIdx.x; e < D * 32; e += NT) {
+            const int dd = e >> 5, sl = w.kv_len - tail0 + (e & 31);
+            if (sl < (nchunks - ctail) * 32) sVt[dd][sl] = 0;
+          }
+          __syncthreads();
+          // commits (tree_inc...cu:335-396): staging row -> depth slot, in
+          // HBM and in the tail (their slots differ from this step's stores:
+          // a coinciding commit was applied by its own launch, kv.C == 0)
+#pragma unroll
+          for (int i = 0; i < CP; ++i) {
+            const int e = threadIdx.x + i * NT, j = e / (2 * D8), r = e % (2 * D8);
+            if (j >= ncm) continue;
+            const int dep = wdp->cm_depth[j], i8 = (r % D8) * 8;
+            if (dep < 0 || dep >= slots) continue;
+            const int ts = dep - tail0;
+            if (r < D8) {
+              *reinterpret_cast<uint4 *>(kc + (((size_t)w.req * heads + h) * slots + dep) * D + i8) =
+                  cmv[i];
+              *reinterpret_cast<uint4 *>(&sKt[ts][i8]) = cmv[i];
+            } else {
+              uint16_t *vt = vc + (((size_t)w.req * heads + h) * D + i8) * slots + dep;
+              const uint32_t vw[4] = {cmv[i].x, cmv[i].y, cmv[i].z, cmv[i].w};
+#pragma unroll
+              for (int jj = 0; jj < 8; ++jj) {
+                const uint16_t v = (uint16_t)(vw[jj >> 1] >> (16 * (jj & 1)));
+                vt[(size_t)jj * slots] = v;
+                sVt[i8 + jj][ts] = v;
+              }
+            }
+          }
+          stamp(6);
         });
     stamp(7);
     __syncthreads();
     stamp(8);
-    kv_store_vt<D, NQ>(w, h, heads, slots, vc, sV, sSlot);
+    // V^T of this step's tokens to HBM from the tail (not waited for)
+    {
+      uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
+      for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
+        const int dd = e / NQ, tt = e % NQ;
+        if (tt >= w.q_count) continue;
+        const int sl = sSlot[tt];
+        if (sl >= 0) vt[(size_t)dd * slots + sl] = sVt[dd][sl - tail0];
+      }
+    }
     stamp(9);
-    // this workgroup's stores become visible to its own loads below (the
-    // (req, head) K/V lines are touched by no other workgroup this step)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
 
   stamp(1);
@@ -529,6 +631,22 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   };
   // wave w takes chunks w, w+NW, ... (two waves per SIMD hide each other's
   // load latency; per-wave double buffering would not fit the registers)
+  // FUSED: chunks from ctail on come from the LDS tail
+  auto load_chunk_lds = [&](int lc, h8 (&kf)[2][KS], h8 (&va)[DT]) {
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      const uint16_t *krow = &sKt[lc * 32 + sub * 16 + (lane & 15)][8 * g];
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) kf[sub][ks] = *reinterpret_cast<const h8 *>(krow + 32 * ks);
+    }
+#pragma unroll
+    for (int t = 0; t < DT; ++t) {
+      const uint16_t *vrow = &sVt[t * 16 + (lane & 15)][lc * 32 + 4 * g];
+      h4 v0 = *reinterpret_cast<const h4 *>(vrow);
+      h4 v1 = *reinterpret_cast<const h4 *>(vrow + 16);
+      va[t] = h8{v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+    }
+  };
   stamp(2);
   for (int c = wave; c < nchunks; c += NW) {
     if (early && c == wave) {
@@ -536,11 +654,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       continue;
     }
     h8 kf[2][KS], va[DT];
-    load_chunk(c, kf, va);
+    if (FUSED && c >= ctail) load_chunk_lds(c - ctail, kf, va);
+    else load_chunk(c, kf, va);
     compute_chunk(c * 32, kf, va);
   }
 
   stamp(3);
+  if (FUSED) __syncthreads();  // the merge buffer reuses the tail's LDS
   // per-query partial sum over the 4 lane groups (same m_run in all four)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {

@@ -516,6 +516,11 @@ struct LlamaGPU : public ffmi_model {
     prof_this_step = prof_level == 1 && (prof_steps++ % prof_every) == 0;
     ffmi_batch_desc desc;
     ps.desc(&desc);
+    // the embedding gather indexes the table by token id: reject bad ids on
+    // the host instead of reading out of bounds on the device
+    for (int t = 0; t < T; ++t)
+      FFMI_CHECK(desc.tokens[t].token_id >= 0 && desc.tokens[t].token_id < c.vocab_size,
+                 FFMI_ERR_INVALID);
     size_t bytes = 0;
     ffmi_status st = ffmi::batch_stage(batch, &desc, &bytes);
     if (st != FFMI_OK) return st;
@@ -529,7 +534,8 @@ struct LlamaGPU : public ffmi_model {
                        !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
-                         batch->commit_overlap ? 1 : 0, batch->one_item_per_req ? 1 : 0,
+                         batch->commit_overlap ? 1 : 0,
+                         (batch->one_item_per_req ? 1 : 0) | (batch->lds_tail ? 2 : 0),
                          batch->max_q, bytes};
       auto it = graphs.find(key);
       if (it == graphs.end()) {

@@ -1,0 +1,59 @@
+"""Per-wave timeline of the verify attention kernel INSIDE the LLaMA-7B
+SpecInfer model (FFMI_ATTN_STAMP=1): the stamps of the last verify-size
+attention launch of one generate (last layer, last verify step), so the
+prologue sees the qkv GEMM's real split-K slabs and commits.
+
+    python scripts/diag_attn_model.py [--layers 4]
+"""
+import argparse
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ.setdefault("FFMI_ATTN_STAMP", "1")
+import bench  # noqa: E402
+import flexflow_amd as fa  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--layers", type=int, default=4)
+    ap.add_argument("--decode", type=int, default=32)
+    args = ap.parse_args()
+    bench.fa = fa
+    cfg = dict(bench.LLAMA_7B, num_layers=args.layers)
+    B, P = 8, 128
+    prompts = bench.make_prompts(B, P - 1, cfg["vocab_size"])
+    kw = dict(max_requests_per_batch=B, max_tokens_per_batch=1024, max_spec_tree_token_num=23,
+              max_sequence_length=512)
+    llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=1024 + 23 * B, max_seq_len=512,
+                   max_tree_tokens=23, weight_seed=20250117)
+    ssm = fa.Model(dict(bench.LLAMA_68M), "beam", max_requests=B, max_tokens=1024 + 23 * B,
+                   max_seq_len=512, max_tree_tokens=23, weight_seed=68)
+    rm = fa.RequestManager(spec_tree_width=(1, 1, 3), **kw)
+    rm.register_ssm_model(ssm)
+    fa.generate(rm, llm, prompts, max_length=P + args.decode, spec=True)
+    L = fa.ffmi.lib()
+    buf = np.zeros((B * 32 * 8, 12), np.int64)
+    m = L.ffmi_debug_attn_stamps(buf.ctypes.data, buf.shape[0])
+    st = buf[:m]
+    t0 = st[:, 0].min()
+    us = lambda a: np.percentile(a * 10 / 1000, [0, 50, 90, 100]).round(2)  # noqa: E731
+    print(f"== in-model verify attention: waves {m}, span {(st[:, 5].max() - t0) * 10 / 1000:.2f} us")
+    print(f"  {'start':18s} p0/50/90/100 {us(st[:, 0] - t0)}")
+    for a, b, nm in [(0, 6, "commits"), (6, 7, "KV update"), (7, 8, "its barrier"),
+                     (8, 9, "V^T stores"), (9, 1, "drain + barrier")]:
+        print(f"    {nm:16s} {us(st[:, b] - st[:, a])}")
+    names = ["start", "prologue", "setup (q, masks)", "key loop", "to merge barrier",
+             "merge + store"]
+    for i in range(2, 6):
+        print(f"  {names[i]:18s} {us(st[:, i] - st[:, i - 1])}")
+    print(f"  {'end':18s} {us(st[:, 5] - t0)}")
+    print("  chunks per item", np.unique(st[:, 11]))
+
+
+if __name__ == "__main__":
+    main()
