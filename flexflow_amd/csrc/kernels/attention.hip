@@ -442,9 +442,16 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
 
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
   __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
+  __shared__ int4 sMrec[FUSED ? NQ : 1];
+  __shared__ int sSlotV[FUSED ? NQ : 1];
+  __shared__ uint64_t sMvis[FUSED ? NQ : 1];
   if (FUSED) {
-    __shared__ int sSlot[NQ];
+    int *sSlot = sSlotV;
     const WorkDev *wdp = &bv.work[blockIdx.x];
+    // the queries' visibility records go out with the prologue's loads and
+    // reach the key loop through LDS (a load there was one more round trip)
+    int4 mrec;
+    uint64_t mvis;
     constexpr int NT = 64 * NW;
     constexpr int D8 = D / 8;
     // cached contents of the tail's first `told` (< 32) slots, which this
@@ -457,6 +464,18 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     // the request's commits (16-B pieces of the staging K and V rows)
     constexpr int CP = (kItemCommits * 2 * D8 + NT - 1) / NT;
     const int ncm = kv.C > 0 ? wdp->ncommit : 0;
+    // commit sources through the scalar cache, with the work item: the
+    // staging loads then wait on no vector load (one round trip, not two)
+    const uint32_t *cs32 = reinterpret_cast<const uint32_t *>(wdp->cm_src);
+    int csrc[CP];  // this thread's commit pieces: source staging rows
+#pragma unroll
+    for (int i = 0; i < CP; ++i) {
+      const int j = min(((int)threadIdx.x + i * NT) / (2 * D8), kItemCommits - 1);
+      uint32_t wd = cs32[0];
+#pragma unroll
+      for (int jj = 1; jj < kItemCommits / 2; ++jj) wd = (j >> 1) == jj ? cs32[jj] : wd;
+      csrc[i] = (int)(int16_t)((j & 1) ? (wd >> 16) : (wd & 0xffffu));
+    }
     uint4 cmv[CP];
     kv_update_item<D, NQ, NT>(
         bv, wdp, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
@@ -466,7 +485,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
           for (int i = 0; i < CP; ++i) {
             const int e = threadIdx.x + i * NT, j = e / (2 * D8), r = e % (2 * D8);
             if (j < ncm) {
-              const int src = wdp->cm_src[j];
+              const int src = csrc[i];
               cmv[i] = *reinterpret_cast<const uint4 *>(
                   kv.stage_rd + (size_t)src * 2 * Hl + (r >= D8 ? Hl : 0) + h * D + (r % D8) * 8);
             }
@@ -483,10 +502,17 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
             if (dd < D && s8 < told)
               tv[i] = *reinterpret_cast<const uint4 *>(vbase + (size_t)dd * slots + tail0 + s8);
           }
+          if ((int)threadIdx.x < NQ) {
+            const ffmi_token_info *ti = &bv.tokens[w.q_start + min((int)threadIdx.x, max(w.q_count - 1, 0))];
+            mrec = make_int4(ti->prefix_len, ti->tree_base, ti->tree_len, 0);
+            mvis = ti->tree_vis;
+          }
           // (issued last: the waits below for the loads above leave it in flight)
           if (early) load_chunk(wave, kf0, va0);
         },
         [&] {  // loads are back: the old tail to LDS, then the commits
+          stamp(10);
+          if ((int)threadIdx.x < NQ) sMrec[threadIdx.x] = mrec, sMvis[threadIdx.x] = mvis;
 #pragma unroll
           for (int i = 0; i < TK; ++i) {
             const int e = threadIdx.x + i * NT, row = e / D8;
@@ -501,6 +527,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
               dst[1] = make_uint2(tv[i].z, tv[i].w);
             }
           }
+          stamp(11);
           // keys past kv_len in the last chunk are masked, but P.V still
           // multiplies their V by 0: zero them (as the cache's never-written
           // slots are); a stored slot among them is written after the barrier
@@ -539,16 +566,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     stamp(7);
     __syncthreads();
     stamp(8);
-    // V^T of this step's tokens to HBM from the tail (not waited for)
-    {
-      uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
-      for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
-        const int dd = e / NQ, tt = e % NQ;
-        if (tt >= w.q_count) continue;
-        const int sl = sSlot[tt];
-        if (sl >= 0) vt[(size_t)dd * slots + sl] = sVt[dd][sl - tail0];
-      }
-    }
     stamp(9);
   }
 
@@ -561,8 +578,13 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   for (int qt = 0; qt < QT; ++qt) {
     const int q = qt * 16 + qi;
     qvalid[qt] = q < w.q_count;
-    const ffmi_token_info ti = bv.tokens[w.q_start + (qvalid[qt] ? q : 0)];
-    pre[qt] = ti.prefix_len, tb[qt] = ti.tree_base, tlen[qt] = ti.tree_len, tv[qt] = ti.tree_vis;
+    if (FUSED) {
+      const int4 mr = sMrec[qvalid[qt] ? q : 0];
+      pre[qt] = mr.x, tb[qt] = mr.y, tlen[qt] = mr.z, tv[qt] = sMvis[qvalid[qt] ? q : 0];
+    } else {
+      const ffmi_token_info ti = bv.tokens[w.q_start + (qvalid[qt] ? q : 0)];
+      pre[qt] = ti.prefix_len, tb[qt] = ti.tree_base, tlen[qt] = ti.tree_len, tv[qt] = ti.tree_vis;
+    }
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks)
       qf[qt][ks] = !qvalid[qt] ? h8{0, 0, 0, 0, 0, 0, 0, 0}
@@ -660,7 +682,18 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   }
 
   stamp(3);
-  if (FUSED) __syncthreads();  // the merge buffer reuses the tail's LDS
+  if (FUSED) {
+    // V^T of this step's tokens to HBM from the tail, by each wave once its
+    // key loop is done (not waited for)
+    uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
+    for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
+      const int dd = e / NQ, tt = e % NQ;
+      if (tt >= w.q_count) continue;
+      const int sl = sSlotV[tt];
+      if (sl >= 0) vt[(size_t)dd * slots + sl] = sVt[dd][sl - tail0];
+    }
+    __syncthreads();  // the merge buffer reuses the tail's LDS
+  }
   // per-query partial sum over the 4 lane groups (same m_run in all four)
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
@@ -717,10 +750,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   if (ST && stp) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stamp(5);
-    unsigned hwid;
-    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hwid));
-    stp[10] = hwid;
-    stp[11] = nchunks;
   }
 }
 

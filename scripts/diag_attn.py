@@ -65,7 +65,7 @@ def main():
                 print(f"    {nm:16s} {us(st[:, b] - st[:, a])}")
         for i in range(1, 6):
             print(f"  {names[i]:18s} {us(st[:, i] - st[:, i - 1])}")
-        print("  chunks per item", np.unique(st[:, 11]))
+        pass
 
 
 if __name__ == "__main__":

@@ -44,7 +44,8 @@ def main():
     us = lambda a: np.percentile(a * 10 / 1000, [0, 50, 90, 100]).round(2)  # noqa: E731
     print(f"== in-model verify attention: waves {m}, span {(st[:, 5].max() - t0) * 10 / 1000:.2f} us")
     print(f"  {'start':18s} p0/50/90/100 {us(st[:, 0] - t0)}")
-    for a, b, nm in [(0, 6, "commits"), (6, 7, "KV update"), (7, 8, "its barrier"),
+    for a, b, nm in [(0, 10, "issue loads"), (10, 11, "wait mrec/tail"), (11, 6, "barrier+commits"),
+                     (6, 7, "KV update"), (7, 8, "its barrier"),
                      (8, 9, "V^T stores"), (9, 1, "drain + barrier")]:
         print(f"    {nm:16s} {us(st[:, b] - st[:, a])}")
     names = ["start", "prologue", "setup (q, masks)", "key loop", "to merge barrier",
@@ -52,7 +53,6 @@ def main():
     for i in range(2, 6):
         print(f"  {names[i]:18s} {us(st[:, i] - st[:, i - 1])}")
     print(f"  {'end':18s} {us(st[:, 5] - t0)}")
-    print("  chunks per item", np.unique(st[:, 11]))
 
 
 if __name__ == "__main__":
