@@ -112,3 +112,14 @@ def ulp_diff(a16, b16):
         u = np.asarray(x, np.float16).view(np.uint16).astype(np.int32)
         return np.where(u & 0x8000, 0x8000 - (u & 0x7FFF), u + 0x8000)
     return np.abs(key(a16) - key(b16))
+
+
+def report(name, **kv):
+    """Append one measured parity figure to gpurun_out/parity_report.jsonl
+    (read back after a GPU run; DESIGN.md quotes it)."""
+    import json
+    import os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    os.makedirs(os.path.join(root, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(root, "gpurun_out", "parity_report.jsonl"), "a") as f:
+        f.write(json.dumps(dict(test=name, **kv)) + "\n")

@@ -17,7 +17,6 @@ Rules:
 
 Measured fractions are appended to gpurun_out/parity_report.jsonl.
 """
-import json
 import os
 
 import numpy as np
@@ -25,7 +24,7 @@ import pytest
 
 import flexflow_amd as fa
 import oracle_lib as O
-from hip_util import ulp_diff
+from hip_util import report, ulp_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -33,10 +32,6 @@ TAGS = ["tiny_d64", "tiny_d128"]
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def report(name, **kv):
-    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "parity_report.jsonl"), "a") as f:
-        f.write(json.dumps(dict(test=name, **kv)) + "\n")
 
 
 def prefill_capture(cfg, seed, prompt, mode="inc", **kw):

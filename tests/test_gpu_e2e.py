@@ -6,14 +6,18 @@ Token parity rule (fp16 model, fp32 accumulation everywhere, different fp32
 summation order on GPU and CPU): the GPU sequence is teacher-forced through
 the oracle; every GPU token must equal the oracle's greedy pick unless the
 oracle's fp16 softmax probabilities of the two tokens are within 2 fp16 ulp
-(a numerical tie), and >= 90% of tokens must be exact picks.
+(a numerical tie), and at most max(1, 2%) of a sequence's tokens may be such
+ties.  Measured (round 2, 34 sequences, 1488 tokens): 1484 exact picks, at
+most one tie per sequence (the fractions go to gpurun_out/parity_report.jsonl).
 """
 import numpy as np
 import pytest
 
 import flexflow_amd as fa
 import oracle_lib as O
-from hip_util import ulp_diff
+import os
+
+from hip_util import report, ulp_diff
 
 pytestmark = pytest.mark.gpu
 
@@ -46,7 +50,9 @@ def check_tokens_vs_oracle(cfg, seed, seq, n_prompt, tie_ulp=2):
         p16 = (p / p.sum()).astype(np.float16)
         assert ulp_diff(p16[g], p16[ids[t]]) <= tie_ulp, (t, g, ids[t], float(p16[g]),
                                                           float(p16[ids[t]]))
-    assert exact >= 0.9 * len(gen), (exact, len(gen))
+    report("tokens_vs_oracle", where=os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0],
+           exact=exact, total=len(gen))
+    assert len(gen) - exact <= max(1, 0.02 * len(gen)), (exact, len(gen))
     return exact
 
 
