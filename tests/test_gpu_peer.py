@@ -92,3 +92,26 @@ def test_peer_tp2_spec_infer_equals_incr():
     inc = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, False, ssm), max_bytes=1 << 20)
     spec = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, True, ssm), max_bytes=1 << 20)
     assert spec[0] == spec[1] == inc[0] == inc[1]
+
+
+# LLaMA-65B widths (configs D/E: hidden 8192, 64 heads of 128, FFN 22016,
+# vocab 32000), one layer, sharded over 8 rank processes exactly as the
+# driver's TP = 8 run shards it: per-rank qkv 3072 x 8192, o 8192 x 1024,
+# gate|up 2 x 2752 x 8192, down 8192 x 2752, lm_head vocab shard 4000 x 8192
+CFG65 = dict(num_layers=1, vocab_size=32000, num_heads=64, num_kv_heads=64, hidden=8192,
+             intermediate=22016, rms_eps=1e-5, rope_theta=10000.0)
+
+
+def test_peer_tp8_llama65b_width_decodes_like_unsharded():
+    """Config D's per-rank shapes end to end: 8 ranks over the xGMI transport
+    (row-parallel halves all-reduced on the second stream, vocab-sharded tail,
+    graphed steps) emit identical tokens on every rank, each an oracle-valid
+    greedy pick of the unsharded model (ties within 2*TP fp16 ulp)."""
+    from test_gpu_e2e import SSM_CFG, check_tokens_vs_oracle, prompts
+    ps = prompts(2, CFG65["vocab_size"], 4, 12, 3)
+    res = run_group(8, PT.model_task, (CFG65, 11, ps, 24, False, SSM_CFG), max_bytes=8 << 20)
+    for r in range(1, 8):
+        assert res[r] == res[0]
+    for p, toks in zip(ps, res[0]):
+        assert len(toks) == 24
+        check_tokens_vs_oracle(CFG65, 11, toks, len(p) + 1, tie_ulp=16)
