@@ -326,7 +326,9 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
 // e.g. the 68M SSM's o/down with 48 tiles) and only when the consumer takes
 // the partial slabs (no reduce pass); keeps >= 4 k-steps per wave.
 static int skinny_split(int T, int N, int K, int epi, bool deferrable) {
-  if (!deferrable || epi || T > 64) return 1;
+  // FFMI_SKINNY_SPLIT=0 keeps every skinny launch unsplit (A/B runs)
+  static const bool off = getenv("FFMI_SKINNY_SPLIT") && atoi(getenv("FFMI_SKINNY_SPLIT")) == 0;
+  if (off || !deferrable || epi || T > 64) return 1;
   const int ntiles = (N + 15) / 16;
   if (ntiles >= 128) return 1;
   const int KT = K / 32;
