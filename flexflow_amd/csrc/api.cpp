@@ -773,6 +773,22 @@ extern "C" ffmi_status ffmi_comm_peer_status(ffmi_comm *c) {
 extern "C" ffmi_status ffmi_comm_peer_attach(ffmi_comm *c, const void *handles) {
   FFMI_CHECK(c && c->peer && handles && !c->peer->attached, FFMI_ERR_INVALID);
   PeerState &p = *c->peer;
+  // one process per GPU of a node: every other device of the group must be
+  // reachable over xGMI before any kernel touches a peer's buffer (a
+  // refused check is an error the caller answers with RCCL, never a fault);
+  // ranks sharing one device (the multi-process tests) need no peer access
+  int ndev = 0, me = 0;
+  FFMI_HIP(hipGetDeviceCount(&ndev));
+  FFMI_HIP(hipGetDevice(&me));
+  if (ndev >= c->nranks)
+    for (int d = 0; d < c->nranks; ++d) {
+      int can = 1;
+      if (d != me) FFMI_HIP(hipDeviceCanAccessPeer(&can, me, d));
+      if (!can) {
+        ffmi_set_last_error("xGMI transport: a peer device is not reachable", __FILE__, __LINE__);
+        return FFMI_ERR_UNSUPPORTED;
+      }
+    }
   for (int r = 0; r < c->nranks; ++r) {
     if (r == c->rank) {
       p.base[r] = p.own;

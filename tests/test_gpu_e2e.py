@@ -7,7 +7,7 @@ summation order on GPU and CPU): the GPU sequence is teacher-forced through
 the oracle; every GPU token must equal the oracle's greedy pick unless the
 oracle's fp16 softmax probabilities of the two tokens are within 2 fp16 ulp
 (a numerical tie), and at most max(1, 2%) of a sequence's tokens may be such
-ties.  Measured (round 2, 34 sequences, 1488 tokens): 1484 exact picks, at
+ties (10% for TP shards, whose all-reduces reorder the sums).  Measured (round 2, 34 sequences, 1488 tokens): 1484 exact picks, at
 most one tie per sequence (the fractions go to gpurun_out/parity_report.jsonl).
 """
 import numpy as np
@@ -32,9 +32,11 @@ def prompts(n, V, lo, hi, seed):
     return [rng.integers(3, V, size=int(rng.integers(lo, hi))).tolist() for _ in range(n)]
 
 
-def check_tokens_vs_oracle(cfg, seed, seq, n_prompt, tie_ulp=2):
+def check_tokens_vs_oracle(cfg, seed, seq, n_prompt, tie_ulp=2, max_tie_frac=0.02):
     """teacher-forced check of seq[n_prompt:] against the oracle; a mismatch
-    must be a tie within tie_ulp fp16 ulp of the two tokens' probabilities."""
+    must be a tie within tie_ulp fp16 ulp of the two tokens' probabilities, and
+    at most max(1, max_tie_frac) of the tokens may be ties (TP shards, whose
+    all-reduces change the summation order, pass a wider bound)."""
     m = O.Model(cfg, seed, fp16=1, max_requests=1, max_seq=len(seq) + 1)
     logits = m.forward(0, np.array(seq[:-1], np.int32), 0)
     gen = seq[n_prompt:]
@@ -52,7 +54,7 @@ def check_tokens_vs_oracle(cfg, seed, seq, n_prompt, tie_ulp=2):
                                                           float(p16[ids[t]]))
     report("tokens_vs_oracle", where=os.environ.get("PYTEST_CURRENT_TEST", "").split(" ")[0],
            exact=exact, total=len(gen))
-    assert len(gen) - exact <= max(1, 0.02 * len(gen)), (exact, len(gen))
+    assert len(gen) - exact <= max(1, max_tie_frac * len(gen)), (exact, len(gen))
     return exact
 
 

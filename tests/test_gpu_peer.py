@@ -80,7 +80,8 @@ def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
         assert res[r] == res[0]
     for p, toks in zip(ps, res[0]):
         assert len(toks) == 56
-        check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp)
+        check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp,
+                               max_tie_frac=0.1)
 
 
 def test_peer_tp2_spec_infer_equals_incr():
@@ -114,4 +115,5 @@ def test_peer_tp8_llama65b_width_decodes_like_unsharded():
         assert res[r] == res[0]
     for p, toks in zip(ps, res[0]):
         assert len(toks) == 24
-        check_tokens_vs_oracle(CFG65, 11, toks, len(p) + 1, tie_ulp=16)
+        check_tokens_vs_oracle(CFG65, 11, toks, len(p) + 1, tie_ulp=16,
+                               max_tie_frac=0.1)

@@ -77,7 +77,8 @@ def test_tp_shards_decode_like_unsharded_model(cfg, tp):
         assert [x.output_tokens for x in res[r]] == [x.output_tokens for x in res[0]]
     for p, x in zip(ps, res[0]):
         assert len(x.output_tokens) == 56
-        check_tokens_vs_oracle(cfg, 11, x.output_tokens, len(p) + 1, tie_ulp=2 * tp)
+        check_tokens_vs_oracle(cfg, 11, x.output_tokens, len(p) + 1, tie_ulp=2 * tp,
+                               max_tie_frac=0.1)
 
 
 def test_tp2_spec_infer_tokens_are_greedy():
@@ -85,4 +86,5 @@ def test_tp2_spec_infer_tokens_are_greedy():
     res = run_tp(LLM_CFG, 11, 2, ps, 60, spec=True)
     assert [x.output_tokens for x in res[1]] == [x.output_tokens for x in res[0]]
     for p, x in zip(ps, res[0]):
-        check_tokens_vs_oracle(LLM_CFG, 11, x.output_tokens, len(p) + 1, tie_ulp=4)
+        check_tokens_vs_oracle(LLM_CFG, 11, x.output_tokens, len(p) + 1, tie_ulp=4,
+                               max_tie_frac=0.1)
