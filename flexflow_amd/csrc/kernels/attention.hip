@@ -99,7 +99,10 @@ __device__ __forceinline__ void st_h4(uint16_t *p, uint16_t a, uint16_t b, uint1
 // where its attention reads them -- no wait for the global stores; V^T then
 // goes to HBM from sVt.  before_stores() runs (in every thread) once the
 // loads are back, before the first store.
-template <int D, int NQ, int NT, class AfterLoads, class BeforeStores>
+// PSRC: 1 = qkv from split-K slabs, 0 = fp16 qkv, -1 = decided at run time
+// by `part` (a compile-time source keeps the two load paths from joining:
+// the join's register copies waited for half of the slab loads).
+template <int D, int NQ, int NT, int PSRC = -1, class AfterLoads, class BeforeStores>
 __device__ __forceinline__ void kv_update_item(
     const BatchView &bv, const WorkDev *__restrict__ wdp, int h, int heads, int slots, int T,
     const uint16_t *__restrict__ qkv, const float *__restrict__ part, int pS, int pNP,
@@ -117,7 +120,9 @@ __device__ __forceinline__ void kv_update_item(
   int tl[U], i0[U];
   // One round trip for every prologue load.  The RoPE positions of the
   // item's tokens come through the scalar cache (16 dwords of the work item,
-  // lgkmcnt), so the RoPE-row loads do not wait on any vector load; the qkv
+  // lgkmcnt; readfirstlane keeps them there -- the per-lane select over them
+  // was folded into a vector load), so the RoPE-row loads do not wait on any
+  // vector load; the qkv
   // slabs (addresses known up front), the RoPE rows and the token records
   // then go out back to back.  (Vector loads complete in issue order: with
   // the positions loaded per lane, the RoPE rows waited for that load and
@@ -125,7 +130,7 @@ __device__ __forceinline__ void kv_update_item(
   const uint32_t *rp32 = reinterpret_cast<const uint32_t *>(wdp->rope_pos);
   uint32_t rpw[FFMI_ATTN_QTILE / 2];
 #pragma unroll
-  for (int j = 0; j < FFMI_ATTN_QTILE / 2; ++j) rpw[j] = rp32[j];
+  for (int j = 0; j < FFMI_ATTN_QTILE / 2; ++j) rpw[j] = __builtin_amdgcn_readfirstlane(rp32[j]);
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int e = min((int)threadIdx.x + u * NT, UNITS - 1);
@@ -137,7 +142,7 @@ __device__ __forceinline__ void kv_update_item(
     const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
                         Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
                         2 * Hl + h * D + i0[u] + HD};
-    if (part) {  // slabs 0 and 1 (slab 0 again when pS == 1: no branch)
+    if (PSRC == 1 || (PSRC < 0 && part)) {  // slabs 0 and 1 (slab 0 again when pS == 1: no branch)
       const float *p1 = part + (pS > 1 ? (size_t)T * pNP : 0);
 #pragma unroll
       for (int c = 0; c < 6; ++c)
@@ -171,7 +176,12 @@ __device__ __forceinline__ void kv_update_item(
     treq[u] = bv.tokens[t].req;
   }
   after_loads();
-  if (!part)
+  // every prologue load is in flight before any of them is consumed: left
+  // alone the scheduler summed the slabs right after they were issued and
+  // gave their registers to the RoPE rows, so each group of loads waited for
+  // the one before it (four round trips instead of one)
+  __builtin_amdgcn_sched_barrier(0);
+  if (PSRC == 0 || (PSRC < 0 && !part))
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -179,7 +189,7 @@ __device__ __forceinline__ void kv_update_item(
         const uint32_t a = __float_as_uint(y[u][c][0]), b = __float_as_uint(y[u][c][1]);
         x[u][c] = f4{h2f(a & 0xffff), h2f(a >> 16), h2f(b & 0xffff), h2f(b >> 16)};
       }
-  if (part) {  // slabs in slice order, then fp16 (partials_value)
+  if (PSRC == 1 || (PSRC < 0 && part)) {  // slabs in slice order, then fp16 (partials_value)
     if (pS > 1)
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -368,7 +378,7 @@ struct KvUpdateArgs {
 // own request's TREE commits and the KV update of its own tokens for its
 // head (kv_update_kernel's work), makes them visible to the workgroup, then
 // attends -- one launch per step instead of two.
-template <int D, int QT, int NW, bool FUSED, bool ST = false>
+template <int D, int QT, int NW, bool FUSED, bool ST = false, int PSRC = -1>
 __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     const char *__restrict__ blob, uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
     uint16_t *__restrict__ vc, uint16_t *__restrict__ out, int heads, int slots, float scale,
@@ -466,18 +476,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     const int ncm = kv.C > 0 ? wdp->ncommit : 0;
     // commit sources through the scalar cache, with the work item: the
     // staging loads then wait on no vector load (one round trip, not two)
+    // (readfirstlane keeps them scalar: a select over the loaded words was
+    // folded into a per-lane load that the staging loads then waited for)
     const uint32_t *cs32 = reinterpret_cast<const uint32_t *>(wdp->cm_src);
+    uint32_t csw[kItemCommits / 2];
+#pragma unroll
+    for (int jj = 0; jj < kItemCommits / 2; ++jj) csw[jj] = __builtin_amdgcn_readfirstlane(cs32[jj]);
     int csrc[CP];  // this thread's commit pieces: source staging rows
 #pragma unroll
     for (int i = 0; i < CP; ++i) {
       const int j = min(((int)threadIdx.x + i * NT) / (2 * D8), kItemCommits - 1);
-      uint32_t wd = cs32[0];
+      uint32_t wd = csw[0];
 #pragma unroll
-      for (int jj = 1; jj < kItemCommits / 2; ++jj) wd = (j >> 1) == jj ? cs32[jj] : wd;
+      for (int jj = 1; jj < kItemCommits / 2; ++jj) wd = (j >> 1) == jj ? csw[jj] : wd;
       csrc[i] = (int)(int16_t)((j & 1) ? (wd >> 16) : (wd & 0xffffu));
     }
     uint4 cmv[CP];
-    kv_update_item<D, NQ, NT>(
+    kv_update_item<D, NQ, NT, PSRC>(
         bv, wdp, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
         qbuf, kc, kv.stage_wr, nullptr, sSlot, sQ, sKt, sVt, tail0,
         [&] {  // after the KV update's own loads: commits, tail, first chunk
@@ -759,9 +774,18 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
                                      int slots, float scale, hipStream_t s, int op, bool fused,
                                      const KvUpdateArgs &kv) {
   const dim3 grid(W, heads);
-#define FFMI_ATT(QT, FU)                                                                     \
-  hipLaunchKernelGGL((attention_kernel<D, QT, 8, FU>), grid, dim3(512), 0, s, blob, qbuf, kc,  \
-                     vc, out, heads, slots, scale, op, kv)
+#define FFMI_ATT(QT, FU)                                                                      \
+  do {                                                                                          \
+    if (!FU)                                                                                    \
+      hipLaunchKernelGGL((attention_kernel<D, QT, 8, false>), grid, dim3(512), 0, s, blob, qbuf, \
+                         kc, vc, out, heads, slots, scale, op, kv);                             \
+    else if (kv.part)                                                                           \
+      hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 1>), grid, dim3(512), 0, s,    \
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
+    else                                                                                        \
+      hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 0>), grid, dim3(512), 0, s,    \
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
+  } while (0)
   if (kv.stamps && D == 128 && max_q > 16) {  // diagnostics build of the verify kernels
     if (fused)
       hipLaunchKernelGGL((attention_kernel<D, 2, 8, true, true>), grid, dim3(512), 0, s, blob,

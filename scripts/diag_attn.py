@@ -20,12 +20,13 @@ from hip_util import Buf, f16  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ctx", type=int, default=128)
+    ap.add_argument("--heads", type=int, default=32, help="heads per rank (4: LLaMA-7B at TP = 8)")
     # one mode per process: fused then split in one process segfaults on the
     # host in the split call (stamp builds only; not understood yet)
     ap.add_argument("--modes", default="fused")
     args = ap.parse_args()
     L = F.lib()
-    R, n, H, D, ctx = 8, 21, 32, 128, args.ctx
+    R, n, H, D, ctx = 8, 21, args.heads, 128, args.ctx
     T = R * n
     cfg = F.AttnCfg(F.ATTN_TREE, H, D, R, 512, 32, T, 1.0 / np.sqrt(D), 10000.0, 1)
     h = ctypes.c_void_p()
