@@ -22,7 +22,7 @@ __device__ __forceinline__ void sfor_impl(F &&f) {
 template <int N, class F>
 __device__ __forceinline__ void sfor(F &&f) { sfor_impl<0, N>(f); }
 
-template <int MTW, int NTW, int PF, int MODE, int ROT, int LAY, int WL = 0, int NTL = 0, int LB = 1>
+template <int MTW, int NTW, int PF, int MODE, int ROT, int LAY, int WL = 0, int NTL = 0, int LB = 1, int WMOD = 0, int NOULD = 0>
 __global__ __launch_bounds__(256, LB) void probe(const uint16_t *__restrict__ X,
                                                 const uint16_t *__restrict__ Wp,
                                                 float *__restrict__ out, int T, int KT,
@@ -38,10 +38,11 @@ __global__ __launch_bounds__(256, LB) void probe(const uint16_t *__restrict__ X,
   const uint16_t *bsrc[PPT];
 #pragma unroll
   for (int p = 0; p < PPT; ++p) {
-    const int t = min(tile0 + min(wave + 4 * p, NTW - 1), NTILES - 1);
+    int t = min(tile0 + min(wave + 4 * p, NTW - 1), NTILES - 1);
+    if (WMOD) t %= WMOD;
     bsrc[p] = WL ? Wp + (size_t)t * 512 + lane * 8 : Wp + (size_t)t * KT * 512 + lane * 8;
   }
-  const size_t wks = WL ? (size_t)NTILES * 512 : 512;
+  const size_t wks = WL ? (size_t)(WMOD ? WMOD : NTILES) * 512 : 512;
   const uint16_t *xrow[MTW];
   size_t xs;
 #pragma unroll
@@ -66,7 +67,7 @@ __global__ __launch_bounds__(256, LB) void probe(const uint16_t *__restrict__ X,
       for (int i = 0; i < MTW; ++i) xq[q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kq * xs);
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
-      if (!(MODE & 8)) bq[q][p] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * wks)) : *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * wks);
+      if (!(MODE & 8) && (!NOULD || NTW % 4 == 0 || wave + 4 * p < NTW)) bq[q][p] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * wks)) : *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kq * wks);
       else bq[q][p] = h8{};
   }
   if (!(MODE & 1))
@@ -109,7 +110,7 @@ __global__ __launch_bounds__(256, LB) void probe(const uint16_t *__restrict__ X,
       for (int i = 0; i < MTW; ++i) xq[Q][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kw * xs);
 #pragma unroll
     for (int p = 0; p < PPT; ++p)
-      if (!(MODE & 8)) bq[Q][p] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * wks)) : *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * wks);
+      if (!(MODE & 8) && (!NOULD || NTW % 4 == 0 || wave + 4 * p < NTW)) bq[Q][p] = NTL ? __builtin_nontemporal_load(reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * wks)) : *reinterpret_cast<const h8 *>(bsrc[p] + (size_t)kw * wks);
     if (!(MODE & 1))
 #pragma unroll
       for (int i = 0; i < MTW; ++i) xq[Q][i] = bq[Q][0];
@@ -131,7 +132,7 @@ __global__ __launch_bounds__(256, LB) void probe(const uint16_t *__restrict__ X,
   out[blockIdx.x * blockDim.x + threadIdx.x] = s;
 }
 
-template <int MTW, int NTW, int PF, int MODE, int ROT, int LAY, int WL = 0, int NTL = 0, int LB = 1>
+template <int MTW, int NTW, int PF, int MODE, int ROT, int LAY, int WL = 0, int NTL = 0, int LB = 1, int WMOD = 0, int NOULD = 0>
 static void run(const uint16_t *X, uint16_t *W, size_t copy_halves, int copies, float *out, int T,
                 int KT) {
   const int ntiles = 1380 / NTW * NTW;
@@ -140,11 +141,11 @@ static void run(const uint16_t *X, uint16_t *W, size_t copy_halves, int copies, 
   hipEventCreate(&a);
   hipEventCreate(&b);
   for (int i = 0; i < copies; ++i)
-    probe<MTW, NTW, PF, MODE, ROT, LAY, WL, NTL, LB><<<wgs, 256>>>(X, W + i * copy_halves, out, T, KT, ntiles);
+    probe<MTW, NTW, PF, MODE, ROT, LAY, WL, NTL, LB, WMOD, NOULD><<<wgs, 256>>>(X, W + i * copy_halves, out, T, KT, ntiles);
   const int iters = 3 * copies;
   hipEventRecord(a);
   for (int i = 0; i < iters; ++i)
-    probe<MTW, NTW, PF, MODE, ROT, LAY, WL, NTL, LB><<<wgs, 256>>>(X, W + (i % copies) * copy_halves, out, T,
+    probe<MTW, NTW, PF, MODE, ROT, LAY, WL, NTL, LB, WMOD, NOULD><<<wgs, 256>>>(X, W + (i % copies) * copy_halves, out, T,
                                                       KT, ntiles);
   hipEventRecord(b);
   hipEventSynchronize(b);
@@ -153,7 +154,7 @@ static void run(const uint16_t *X, uint16_t *W, size_t copy_halves, int copies, 
   const double us = ms * 1000.0 / iters;
   const double wbytes = (MODE & 8) ? 0.0 : (double)ntiles * KT * 1024;
   const double xbytes = (MODE & 1) ? (double)wgs * 4 * MTW * KT * 1024 : 0.0;
-  printf("LB %d NTL %d NTW %2d PF %d mode %2d rot %d lay %d wl %d: %7.2f us  %5.1f GB/s/CU in (W+X)\n", LB, NTL, NTW, PF, MODE,
+  printf("NOULD %d WMOD %d LB %d NTL %d NTW %2d PF %d mode %2d rot %d lay %d wl %d: %7.2f us  %5.1f GB/s/CU in (W+X)\n", NOULD, WMOD, LB, NTL, NTW, PF, MODE,
          ROT, LAY, WL, us, (wbytes + xbytes) / us / 1e3 / wgs);
 }
 
@@ -186,10 +187,12 @@ int main(int argc, char **argv) {
   hipMalloc(&out, 64 << 20);
 #define R(NTW, PF, MODE, ROT, LAY) run<3, NTW, PF, MODE, ROT, LAY>(X, W, copy_halves, copies, out, T, KT)
 #define RW(NTW, PF, MODE, ROT, WL) run<3, NTW, PF, MODE, ROT, 0, WL>(X, W, copy_halves, copies, out, T, KT)
-#define RN(NTW, PF, MODE, ROT, WL, NL, LB) run<3, NTW, PF, MODE, ROT, 0, WL, NL, LB>(X, W, copy_halves, copies, out, T, KT)
-  RN(6, 4, 7, 0, 0, 1, 2);
-  RN(6, 4, 7, 0, 1, 1, 2);
-  RN(6, 4, 0, 0, 1, 1, 2);
-  RN(6, 4, 9, 0, 1, 1, 2);
+#define RU(MODE, NU) run<3, 6, 4, MODE, 0, 0, 1, 1, 2, 0, NU>(X, W, copy_halves, copies, out, T, KT)
+  RU(7, 0);
+  RU(7, 1);
+  RU(7, 0);
+  RU(7, 1);
+  RU(1, 0);
+  RU(1, 1);
   return 0;
 }
