@@ -16,6 +16,8 @@
 #include <algorithm>
 #include <chrono>
 
+void ffmi_set_last_error(const char *msg, const char *file, int line);  // api.cpp
+
 namespace ffmi {
 
 double now_us() {
@@ -297,6 +299,13 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
           traverse_verify_tree(guid, dfs_tree_inputs.at(guid), tree_outputs);
       stats.tokens_committed += (long)verified_tokens.size();
       stats.request_verifies++;
+      // The reference keeps no SpecInfer ttft (its output record has none,
+      // :1303-1311); recorded here for the Python results only.
+      ProfileInfo &pi = profiling_requests[guid];
+      if (!pi.first_token_time_set) {
+        pi.first_token_time = now_us();
+        pi.first_token_time_set = true;
+      }
       if ((int)(verified_tokens.size() + request.tokens.size()) >= request.max_length) {
         for (const auto &tp : verified_tokens)
           if (tp.second < request.max_length) request.tokens.push_back(tp.first);
@@ -346,7 +355,10 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
       new_bc.request_completed[i] = false;
       new_bc.request_running[i] = false;
       num_active_req++;
-      assert(request.ssm_cache_size == request.initial_len);
+      // The reference asserts here (:1425): a prompt the SSM could not load
+      // within one init + MAX_BEAM_DEPTH beam batches while the LLM still
+      // loads it in chunks.  Reported as an error, not an abort.
+      if (request.ssm_cache_size != request.initial_len) ssm_prompt_behind = true;
       auto &R = new_bc.requestsInfo[i];
       R.first_token_depth_in_request = request.ssm_cache_size;
       R.first_token_offset_in_batch = new_bc.num_tokens;
@@ -925,7 +937,16 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   std::vector<BeamSearchBatchConfig> *beam_vec = new std::vector<BeamSearchBatchConfig>();
   ffmi_status st = FFMI_OK;
   while (!all_done()) {
+    ssm_prompt_behind = false;
     beam_vec->assign(ssm_models.size(), prepare_next_batch_init(*tree_bc, *tree_ir, 0));
+    if (ssm_prompt_behind) {
+      ffmi_set_last_error(
+          "SpecInfer: the SSM loaded less of a prompt than the LLM (prompt longer than one "
+          "init + MAX_BEAM_DEPTH beam batches can hold; raise max_tokens_per_batch)",
+          __FILE__, __LINE__);
+      st = FFMI_ERR_UNSUPPORTED;
+      break;
+    }
     if (all_done()) break;
     for (size_t s = 0; s < ssm_models.size() && st == FFMI_OK; s++) {
       for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {

@@ -152,6 +152,9 @@ class RequestManager {
   int bos_token_id = 1;
   std::vector<int> eos_token_ids;
   bool verbose = false;
+  // set by prepare_next_batch_init when a pending request's SSM prompt load
+  // fell behind the LLM's (the reference asserts there, request_manager.cc:1425)
+  bool ssm_prompt_behind = false;
   std::string output_filepath;
   Detokenizer detok = nullptr;
   void *detok_ctx = nullptr;

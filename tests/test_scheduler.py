@@ -114,8 +114,58 @@ def test_spec_infer_step_efficiency():
         assert r.output_tokens == expected(p, 100, V)
     assert s_inc.llm_steps >= 1.5 * s_spec.llm_steps
     # with a perfect SSM every verify accepts a full 8-deep branch + bonus
-    per_req = [r.llm_decoding_steps for r in res]
-    assert max(per_req) < 20
+    mv = 64 + 23 * 4
+    assert sum(len(r.input_tokens) for r in res) <= mv - len(res)  # one prompt-load step each
+    for r in res:
+        assert len(r.input_tokens) <= 64  # the SSM loads each prompt in its admission batch
+        assert r.llm_decoding_steps == expected_verify_steps(len(r.input_tokens), 100, 64, 4)
+
+
+def expected_verify_steps(in_len, max_length, max_tokens, batch=1, tree_tokens=23):
+    """Per-request llm_decoding_steps of a one-request SpecInfer run whose SSM
+    always agrees with the LLM, restated from the reference's accounting:
+    0 at admission (request_manager.cc:1488) and +1 per verify batch the
+    request is in (:1958).
+      * The LLM loads the prompt in chunks of the verify budget
+        (max_tokens + tree_tokens x batch, :152-156) minus one slot per waiting
+        request (:1938-1946, :2137-2141); the last chunk yields the first new
+        token.
+      * Each later verify commits the full MAX_BEAM_DEPTH (8) branch plus the
+        bonus token, the depth capped by the tokens left (:1355-1369) --
+      * unless the SSM loaded the prompt over three or more beam batches
+        (max_tokens at admission, then max_tokens - 1 each): the reference
+        feeds every beam prompt chunk the LAST n tokens of the request, not
+        the ones at its depths (`request.tokens[size - num_tokens_in_batch +
+        j]`, :1873-1875), which is right only for the final chunk; a middle
+        chunk caches the wrong ids, and (hash model) the SSM never agrees
+        again: one token per verify.  Reproduced, not fixed."""
+    chunks = -(-in_len // (max_tokens + tree_tokens * batch - 1))
+    left = max(0, max_length - (in_len + 1))
+    per_verify = 1 if in_len > 2 * max_tokens - 1 else 9
+    return chunks + -(-left // per_verify)
+
+
+@pytest.mark.parametrize("plen,max_length,max_tokens", [
+    (5, 30, 64), (5, 64, 64), (5, 100, 64), (20, 30, 64), (20, 90, 64), (40, 50, 64),
+    (5, 100, 16), (14, 60, 16), (20, 60, 16), (29, 60, 16),  # SSM loads in <= 2 batches
+    (30, 32, 8), (50, 100, 8), (45, 80, 16), (90, 120, 16)])  # >= 3: wrong SSM prompt
+def test_spec_infer_llm_decoding_steps_per_request(plen, max_length, max_tokens):
+    ps = [list(range(3, 3 + plen))]
+    res, st = run_spec(ps, max_length, batch=1, max_tokens=max_tokens, disagree=0)
+    r = res[0]
+    assert r.output_tokens == expected(ps[0], max_length, V)
+    want = expected_verify_steps(len(r.input_tokens), max_length, max_tokens)
+    assert r.llm_decoding_steps == want
+    assert st.llm_steps == want  # one request: one verify launch per step
+    assert r.ttft_us > 0  # from registration; latency_us counts from admission
+
+
+def test_spec_infer_ssm_prompt_behind_is_an_error():
+    # max_tokens 8: the SSM loads 8 + 8 x 7 = 64 prompt tokens per iteration,
+    # the LLM 30 per verify; a 71-token prompt trips the reference's assert
+    # (request_manager.cc:1425) -- here a reported error, not an abort
+    with pytest.raises(fa.ffmi.FFMIError, match="SSM loaded less"):
+        run_spec([list(range(3, 73))], 100, batch=1, max_tokens=8, disagree=0)
 
 
 def test_request_limits_rejected():
