@@ -295,6 +295,12 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
   }
 }
 
+// Wave-wide reductions on DPP / permlane (device library), not LDS
+// bpermute shuffles: the result is uniform across the wave.
+extern "C" __device__ float __ockl_wfred_max_f32(float);
+extern "C" __device__ double __ockl_wfred_add_f64(double);
+extern "C" __device__ unsigned long long __ockl_wfred_max_u64(unsigned long long);
+
 // Register-resident variant: one TPB-thread workgroup per row reads the row
 // ONCE as 16-B vectors (NV per thread) and keeps it in registers.
 //  * S = float(sum of exp(x_i - M) accumulated in double): the oracle's
@@ -306,14 +312,20 @@ __global__ __launch_bounds__(256) void softmax_topk_kernel(
 //    M + log(boundary * S).  That threshold (lowered by a margin that covers
 //    the float error of exp/div/log) excludes all but a handful of logits, and
 //    the 32000 exp + correctly rounded divisions of a full p pass go away.
-//  * k rounds of a block-wide (p desc, idx asc) selection over the candidates.
+//  * The candidates' (p desc, idx asc) keys go to an LDS list; one wave picks
+//    the k best (k wave reductions, no workgroup barrier).  More than kCand
+//    candidates (flat rows, planted ties) fall back to k rounds of a
+//    workgroup-wide selection over the registers.
 template <int TPB, int NV>
 __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
     float *__restrict__ probs) {
   constexpr int NW = TPB / 64;
-  // ONE shared array: wave maxima / sums / selection keys
+  constexpr int kCand = 128;
+  // wave maxima / sums / selection keys, and the candidate list
   __shared__ double sh[NW + 2];
+  __shared__ unsigned long long cand[kCand];
+  __shared__ unsigned ncand;
   float *fsh = reinterpret_cast<float *>(sh);
   unsigned long long *ksh = reinterpret_cast<unsigned long long *>(sh);
   const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -325,6 +337,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     const int i = v * TPB + tid;
     r[v] = i < nvec ? x[i] : make_uint4(0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u);
   }
+  if (tid == 0) ncand = 0;
   auto elem = [&](int v, int e) -> float {
     const uint32_t w = (&r[v].x)[e >> 1];
     return h2f_((uint16_t)((e & 1) ? (w >> 16) : (w & 0xffffu)));
@@ -334,8 +347,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   for (int v = 0; v < NV; ++v)
 #pragma unroll
     for (int e = 0; e < 8; ++e) mx = fmaxf(mx, elem(v, e));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+  mx = __ockl_wfred_max_f32(mx);
   if (lane == 0) fsh[wv] = mx;
   __syncthreads();
   float wmax[NW];
@@ -372,8 +384,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     if (v * TPB + tid < nvec)
 #pragma unroll
       for (int e = 0; e < 8; ++e) se += (double)__expf(elem(v, e) - M);
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) se += __shfl_xor(se, o);
+  se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
   double sd = 0.0;
@@ -391,8 +402,42 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
       thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
     }
   }
-  __syncthreads();
   // keys: (p + 1) << 32 | ~idx, 0 = not a candidate / taken
+  auto key_of = [&](float xv, unsigned i) -> unsigned long long {
+    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
+  };
+  auto emit = [&](int rd, unsigned long long b) {
+    ids[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
+  };
+#pragma unroll
+  for (int v = 0; v < NV; ++v)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float xv = elem(v, e);
+      const unsigned i = (unsigned)((v * TPB + tid) * 8 + e);
+      if (xv >= thr && (int)i < V) {
+        const unsigned slot = atomicAdd(&ncand, 1u);
+        if (slot < (unsigned)kCand) cand[slot] = key_of(xv, i);
+      }
+    }
+  __syncthreads();
+  const unsigned n = ncand;
+  if (n <= (unsigned)kCand) {
+    if (wv == 0) {  // keys are distinct (they hold the index)
+      unsigned long long a = (unsigned)lane < n ? cand[lane] : 0ull;
+      unsigned long long b = (unsigned)(lane + 64) < n ? cand[lane + 64] : 0ull;
+      for (int rd = 0; rd < k; ++rd) {
+        const unsigned long long best = __ockl_wfred_max_u64(a > b ? a : b);
+        if (lane == 0) emit(rd, best);
+        if (a == best) a = 0ull;
+        if (b == best) b = 0ull;
+      }
+    }
+    return;
+  }
+  // many candidates: k rounds of a workgroup-wide selection
   for (int rd = 0; rd < k; ++rd) {
     unsigned long long best = 0;
 #pragma unroll
@@ -402,17 +447,11 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
         const float xv = elem(v, e);
         const unsigned i = (unsigned)((v * TPB + tid) * 8 + e);
         if (xv >= thr && (int)i < V) {
-          const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
-          const unsigned long long key =
-              ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
+          const unsigned long long key = key_of(xv, i);
           best = key > best ? key : best;
         }
       }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      unsigned long long other = __shfl_xor(best, o);
-      best = other > best ? other : best;
-    }
+    best = __ockl_wfred_max_u64(best);
     if (lane == 0) ksh[wv] = best;
     __syncthreads();
     unsigned long long b = ksh[0];
@@ -420,10 +459,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     for (int q = 1; q < NW; ++q) b = ksh[q] > b ? ksh[q] : b;
     __syncthreads();
     const unsigned idx = 0xffffffffu - (unsigned)(b & 0xffffffffu);
-    if (tid == 0) {
-      ids[(size_t)row * k + rd] = (int)idx;
-      if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
-    }
+    if (tid == 0) emit(rd, b);
     if (rd + 1 < k && (idx >> 3) % TPB == (unsigned)tid) {  // owner marks it taken (-inf)
 #pragma unroll
       for (int v = 0; v < NV; ++v)
@@ -441,15 +477,31 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
                          float *probs, hipStream_t s) {
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4) return hipErrorInvalidValue;
-  const int nv = (V / 8 + 1023) / 1024;
+  // workgroup width (A/B: FFMI_TOPK_TPB = 256 / 512 / 1024)
+  static const int tpb = [] {
+    const char *e = getenv("FFMI_TOPK_TPB");
+    const int v = e ? atoi(e) : 1024;
+    return v == 256 || v == 512 ? v : 1024;
+  }();
+  const int nv = (V / 8 + tpb - 1) / tpb;
   // (NV = 8 at 1024 threads would spill: larger vocabularies take the loop kernel)
-  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv <= 4) {
-#define FFMI_SMR(NV)                                                                        \
-  hipLaunchKernelGGL((softmax_topk_reg_kernel<1024, NV>), dim3(T), dim3(1024), 0, s, logits, V, \
+  if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv * tpb <= 4096) {
+#define FFMI_SMR(TPB, NV)                                                                  \
+  hipLaunchKernelGGL((softmax_topk_reg_kernel<TPB, NV>), dim3(T), dim3(TPB), 0, s, logits, V, \
                      k, ids, probs)
-    if (nv <= 1) FFMI_SMR(1);
-    else if (nv <= 2) FFMI_SMR(2);
-    else FFMI_SMR(4);
+    if (tpb == 256) {
+      if (nv <= 4) FFMI_SMR(256, 4);
+      else if (nv <= 8) FFMI_SMR(256, 8);
+      else FFMI_SMR(256, 16);
+    } else if (tpb == 512) {
+      if (nv <= 2) FFMI_SMR(512, 2);
+      else if (nv <= 4) FFMI_SMR(512, 4);
+      else FFMI_SMR(512, 8);
+    } else {
+      if (nv <= 1) FFMI_SMR(1024, 1);
+      else if (nv <= 2) FFMI_SMR(1024, 2);
+      else FFMI_SMR(1024, 4);
+    }
 #undef FFMI_SMR
   } else {
     hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
