@@ -263,6 +263,29 @@ def test_softmax_topk_chunked_ties(T, V):
         assert ids.get().tolist() == O.softmax_argmax(logits.astype(np.float32), fp16=1)[0].tolist()
 
 
+@pytest.mark.parametrize("nties", [2, 63, 64, 65, 127, 128, 129, 700])
+def test_softmax_topk_candidate_list_capacity(nties):
+    """The register kernel puts the candidates' keys in a 128-entry LDS list
+    read by one wave (two keys per lane); more candidates fall back to
+    workgroup-wide rounds.  Rows with nties equal maxima (and, row 3, half of
+    them 2^-7 lower: fp16 p collapses them) on either side of 64 and 128."""
+    rng = np.random.default_rng(nties)
+    T, V = 4, 32000
+    logits = f16(rng.standard_normal((T, V)))
+    for t in range(T):
+        idx = rng.choice(V, nties, replace=False)
+        logits[t, idx] = f16(7.0 + t)
+        if t == 3:
+            logits[t, idx[: nties // 2]] = f16(10.0 - 2 ** -7)
+    lb = Buf(logits)
+    for k in (1, 3, 4):
+        ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+        F.check(L.ffmi_arg_topk(lb.ptr, T, V, k, ids.ptr, pr.ptr, None))
+        rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+        assert np.array_equal(ids.get(), rid), (k, ids.get(), rid)
+        np.testing.assert_array_equal(pr.get(), rp)
+
+
 # ---------------------------------------------------------------- attention
 def pack_act_np(X):
     """numpy twin of ffmi_pack_activations: [T][K] -> [T/16][K/32][64 lanes][8]."""
