@@ -786,13 +786,19 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 0>), grid, dim3(512), 0, s,    \
                          blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
   } while (0)
-  if (kv.stamps && D == 128 && max_q > 16) {  // diagnostics build of the verify kernels
-    if (fused)
-      hipLaunchKernelGGL((attention_kernel<D, 2, 8, true, true>), grid, dim3(512), 0, s, blob,
-                         qbuf, kc, vc, out, heads, slots, scale, op, kv);
-    else
-      hipLaunchKernelGGL((attention_kernel<D, 2, 8, false, true>), grid, dim3(512), 0, s, blob,
-                         qbuf, kc, vc, out, heads, slots, scale, op, kv);
+  if (kv.stamps && D == 128) {  // diagnostics build of the verify / decode kernels
+#define FFMI_ATT_ST(QT)                                                                         \
+  do {                                                                                          \
+    if (fused)                                                                                  \
+      hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, true>), grid, dim3(512), 0, s, blob,  \
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv);                       \
+    else                                                                                        \
+      hipLaunchKernelGGL((attention_kernel<D, QT, 8, false, true>), grid, dim3(512), 0, s, blob, \
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv);                       \
+  } while (0)
+    if (max_q > 16) FFMI_ATT_ST(2);
+    else FFMI_ATT_ST(1);
+#undef FFMI_ATT_ST
     return hipGetLastError();
   }
   if (max_q <= 16) {
@@ -806,7 +812,7 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
   return hipGetLastError();
 }
 
-// FFMI_ATTN_STAMP=1: verify-size launches record a per-wave timeline
+// FFMI_ATTN_STAMP=1: d = 128 launches record a per-wave timeline
 // {start, after prologue, before k-loop, after k-loop, after merge barrier,
 // end, [fused] after commits, after KV update, after its barrier, after the
 // V^T stores, HW_ID, chunks} (100 MHz realtime) for ffmi_debug_attn_stamps.
