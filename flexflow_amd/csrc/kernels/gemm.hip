@@ -454,7 +454,9 @@ __device__ __forceinline__ void mid_store(const f4 (&acc)[MTW][NTW], uint16_t *_
 }
 
 // Diagnostic stamps (FFMI_GEMM_STAMP=1 builds only): per wave
-// {realtime start, after prologue, after k-loop, end, HW_ID, XCC_ID}, 100 MHz.
+// {realtime start, after prologue, after k-loop, end, HW_ID, XCC_ID, core-clock
+// counter (s_memtime) after prologue, after k-loop}; realtime is 100 MHz, so
+// the k-loop's clock = d(memtime) / d(realtime) x 100 MHz.
 __device__ long long *g_gemm_stamps;
 __device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrealtime(); }
 
@@ -464,7 +466,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
     int NTILES, int S, int yp, size_t wts, size_t wks) {
-  long long st0 = 0, st1 = 0, st2 = 0;
+  long long st0 = 0, st1 = 0, st2 = 0, ck1 = 0, ck2 = 0;
   if (STAMP) st0 = rt_now();
   static_assert(NTW % 2 == 0, "gate/up tiles come in pairs");
   static_assert(PF >= 2, "ring depth");
@@ -535,7 +537,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     for (int p = 0; p < PPT; ++p)
       if (NTW % 4 == 0 || bj[p] < NTW) sB[0][bj[p]][lane] = bq[0][p];
     __syncthreads();
-    if (STAMP) st1 = rt_now();
+    if (STAMP) st1 = rt_now(), ck1 = __builtin_amdgcn_s_memtime();
     // one k-step on ring slot Q; MFMAs read the slot in place, then it is
     // refilled (a copy would rotate the ring through fresh registers and
     // force vmcnt drains at the loop back-edge)
@@ -571,7 +573,7 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     });
   };
   if (kb < ke) kloop(std::integral_constant<int, MTW>{});
-  if (STAMP) st2 = rt_now();
+  if (STAMP) st2 = rt_now(), ck2 = __builtin_amdgcn_s_memtime();
 
   mid_store<MTW, NTW, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0, m0, lane, yp);
   if (STAMP) {
@@ -582,8 +584,9 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
     if (lane == 0 && g_gemm_stamps) {
       const long b = blockIdx.x + (long)gridDim.x * (blockIdx.y + (long)gridDim.y * blockIdx.z);
-      long long *d = g_gemm_stamps + (b * 4 + wave) * 6;
+      long long *d = g_gemm_stamps + (b * 4 + wave) * 8;
       d[0] = st0; d[1] = st1; d[2] = st2; d[3] = st3; d[4] = hwid; d[5] = xcc;
+      d[6] = ck1; d[7] = ck2;
     }
   }
 }
@@ -862,13 +865,13 @@ hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStr
   return hipGetLastError();
 }
 
-// diagnostics: stamps of the last FFMI_GEMM_STAMP launch (6 int64 per wave)
+// diagnostics: stamps of the last FFMI_GEMM_STAMP launch (8 int64 per wave)
 long gemm_debug_stamps(long long *dst, long max_waves) {
   long long *buf = stamp_buf();
   const long n = g_stamp_entries < max_waves ? g_stamp_entries : max_waves;
   if (!buf || n <= 0) return 0;
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpy(dst, buf, (size_t)n * 6 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+  if (hipMemcpy(dst, buf, (size_t)n * 8 * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
     return -1;
   return n;
 }

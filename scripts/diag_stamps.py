@@ -33,7 +33,7 @@ for name, N, K, T in [("qkv", 12288, 4096, 168), ("down", 4096, 11008, 168),
     for i in range(len(copies)):
         F.check(L.ffmi_linear(X.ptr, copies[i].ptr, Y.ptr, T, N, K, F.X_PACKED, None))
     F.check(L.ffmi_linear(X.ptr, copies[0].ptr, Y.ptr, T, N, K, F.X_PACKED, None))
-    buf = np.zeros((1 << 16, 6), np.int64)
+    buf = np.zeros((1 << 16, 8), np.int64)
     n = L.ffmi_debug_gemm_stamps(buf.ctypes.data, buf.shape[0])
     st = buf[:n]
     t0 = st[:, 0].min()
