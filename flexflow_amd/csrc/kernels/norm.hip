@@ -238,71 +238,18 @@ hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out, 
   return hipGetLastError();
 }
 
-// softmax (fp16 output, softmax.cu:262-288) + ArgMax (argmax.cu:62-100) /
-// ArgTopK (arg_topk.cu:339-448).  p_i = half(exp(x_i - max) / sum); the
-// greedy pick is the lowest index of the largest p_i (ties created by the
-// fp16 rounding resolve exactly as cub ArgMax / the top-k heap do).  k
-// rounds of a block-wide (p desc, idx asc) selection.
-__global__ __launch_bounds__(256) void softmax_topk_kernel(
-    const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
-    float *__restrict__ probs) {
-  __shared__ float fscratch[4];
-  __shared__ unsigned long long kscratch[4];
-  const int row = blockIdx.x;
-  const uint16_t *x = logits + (size_t)row * V;
-  float mx = -INFINITY;
-  for (int i = threadIdx.x; i < V; i += 256) mx = fmaxf(mx, h2f_(x[i]));
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-  if ((threadIdx.x & 63) == 0) fscratch[threadIdx.x >> 6] = mx;
-  __syncthreads();
-  mx = fmaxf(fmaxf(fscratch[0], fscratch[1]), fmaxf(fscratch[2], fscratch[3]));
-  __syncthreads();
-  // float exponentials summed in double: S = the oracle's float(double sum)
-  __shared__ double dscratch[4];
-  double se = 0.0;
-  for (int i = threadIdx.x; i < V; i += 256) se += (double)expf(h2f_(x[i]) - mx);
-  const float sum = (float)block_sum256(se, dscratch);
-  int chosen[4] = {-1, -1, -1, -1};
-  for (int r = 0; r < k; ++r) {
-    // key = (p bits << 32) | (~idx): max key = largest p, lowest index
-    unsigned long long best = 0;
-    for (int i = threadIdx.x; i < V; i += 256) {
-      bool taken = false;
-      for (int q = 0; q < r; ++q) taken |= (chosen[q] == i);
-      if (taken) continue;
-      const uint16_t p = f2h_(__fdiv_rn(expf(h2f_(x[i]) - mx), sum));
-      const unsigned long long key =
-          ((unsigned long long)p << 32) | (unsigned long long)(0xffffffffu - (unsigned)i);
-      best = key > best ? key : best;
-    }
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      unsigned long long other = __shfl_xor(best, o);
-      best = other > best ? other : best;
-    }
-    if ((threadIdx.x & 63) == 0) kscratch[threadIdx.x >> 6] = best;
-    __syncthreads();
-    unsigned long long b = kscratch[0];
-    for (int q = 1; q < 4; ++q) b = kscratch[q] > b ? kscratch[q] : b;
-    __syncthreads();
-    const int idx = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
-    chosen[r] = idx;
-    if (threadIdx.x == 0) {
-      ids[(size_t)row * k + r] = idx;
-      if (probs) probs[(size_t)row * k + r] = h2f_((uint16_t)(b >> 32));
-    }
-  }
-}
-
 // Wave-wide reductions on DPP / permlane (device library), not LDS
 // bpermute shuffles: the result is uniform across the wave.
 extern "C" __device__ float __ockl_wfred_max_f32(float);
 extern "C" __device__ double __ockl_wfred_add_f64(double);
 extern "C" __device__ unsigned long long __ockl_wfred_max_u64(unsigned long long);
 
-// Register-resident variant: one TPB-thread workgroup per row reads the row
-// ONCE as 16-B vectors (NV per thread) and keeps it in registers.
+// softmax (fp16 output, softmax.cu:262-288) + ArgMax (argmax.cu:62-100) /
+// ArgTopK (arg_topk.cu:339-448), register-resident: one TPB-thread workgroup
+// per row reads the row ONCE as 16-B vectors (NV per thread) and keeps it in
+// registers.  p_i = half(exp(x_i - max) / S); the pick is the lowest index of
+// the largest p_i (ties created by the fp16 rounding resolve exactly as cub
+// ArgMax / the top-k heap do).
 //  * S = float(sum of exp(x_i - M) accumulated in double): the oracle's
 //    float(double sum), whatever the summation order.
 //  * p_i is computed only for CANDIDATES: p is non-decreasing in x, and the
@@ -473,6 +420,131 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   }
 }
 
+// softmax (fp16 output, softmax.cu:262-288) + ArgMax (argmax.cu:62-100) /
+// ArgTopK (arg_topk.cu:339-448) for rows the register kernel does not take
+// (a vocabulary not a multiple of 8, unaligned rows, V > 32768 such as
+// LLaMA-3's 128256): the same rule -- p_i = half(exp(x_i - max) / S), S =
+// float(double sum), (p desc, index asc) -- in three strided passes over the
+// row (max and wave maxima, sum, candidates; the second and third hit L2),
+// the candidate threshold and LDS list of softmax_topk_reg_kernel below, and
+// k workgroup-wide rounds over the row only when more than kCand logits are
+// candidates.
+template <int TPB>
+__global__ __launch_bounds__(TPB) void softmax_topk_kernel(
+    const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
+    float *__restrict__ probs) {
+  constexpr int NW = TPB / 64;
+  constexpr int kCand = 128;
+  __shared__ double sh[NW + 2];
+  __shared__ unsigned long long cand[kCand];
+  __shared__ unsigned ncand;
+  float *fsh = reinterpret_cast<float *>(sh);
+  unsigned long long *ksh = reinterpret_cast<unsigned long long *>(sh);
+  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const uint16_t *x = logits + (size_t)row * V;
+  if (tid == 0) ncand = 0;
+  float mx = -INFINITY;
+  for (int i = tid; i < V; i += TPB) mx = fmaxf(mx, h2f_(x[i]));
+  mx = __ockl_wfred_max_f32(mx);
+  if (lane == 0) fsh[wv] = mx;
+  __syncthreads();
+  float wmax[NW];
+#pragma unroll
+  for (int q = 0; q < NW; ++q) wmax[q] = fsh[q];
+  __syncthreads();
+  float M = wmax[0];
+#pragma unroll
+  for (int q = 1; q < NW; ++q) M = fmaxf(M, wmax[q]);
+  // L = k-th largest wave maximum: the waves' index sets are disjoint, so it
+  // is a lower bound of the row's k-th largest logit
+  float L = -INFINITY;
+  {
+    float top[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      float v = wmax[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float hi = fmaxf(top[j], v), lo = fminf(top[j], v);
+        top[j] = hi, v = lo;
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (j == k - 1) L = top[j];
+  }
+  double se = 0.0;
+  for (int i = tid; i < V; i += TPB) se += (double)__expf(h2f_(x[i]) - M);
+  se = __ockl_wfred_add_f64(se);
+  if (lane == 0) sh[wv] = se;
+  __syncthreads();
+  double sd = 0.0;
+#pragma unroll
+  for (int q = 0; q < NW; ++q) sd += sh[q];
+  const float S = (float)sd;
+  float thr = -3.402823466e38f;
+  {
+    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    if (pL > 1) {
+      const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
+      thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
+    }
+  }
+  auto key_of = [&](float xv, unsigned i) -> unsigned long long {
+    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
+  };
+  auto emit = [&](int rd, unsigned long long b) {
+    ids[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
+  };
+  for (int i = tid; i < V; i += TPB) {
+    const float xv = h2f_(x[i]);
+    if (xv >= thr) {
+      const unsigned slot = atomicAdd(&ncand, 1u);
+      if (slot < (unsigned)kCand) cand[slot] = key_of(xv, (unsigned)i);
+    }
+  }
+  __syncthreads();
+  const unsigned n = ncand;
+  if (n <= (unsigned)kCand) {
+    if (wv == 0) {
+      unsigned long long a = (unsigned)lane < n ? cand[lane] : 0ull;
+      unsigned long long b = (unsigned)(lane + 64) < n ? cand[lane + 64] : 0ull;
+      for (int rd = 0; rd < k; ++rd) {
+        const unsigned long long best = __ockl_wfred_max_u64(a > b ? a : b);
+        if (lane == 0) emit(rd, best);
+        if (a == best) a = 0ull;
+        if (b == best) b = 0ull;
+      }
+    }
+    return;
+  }
+  int chosen[4] = {-1, -1, -1, -1};
+  for (int rd = 0; rd < k; ++rd) {
+    unsigned long long best = 0;
+    for (int i = tid; i < V; i += TPB) {
+      const float xv = h2f_(x[i]);
+      if (xv < thr) continue;
+      bool taken = false;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) taken |= (q < rd && chosen[q] == i);
+      if (taken) continue;
+      const unsigned long long key = key_of(xv, (unsigned)i);
+      best = key > best ? key : best;
+    }
+    best = __ockl_wfred_max_u64(best);
+    if (lane == 0) ksh[wv] = best;
+    __syncthreads();
+    unsigned long long b = ksh[0];
+#pragma unroll
+    for (int q = 1; q < NW; ++q) b = ksh[q] > b ? ksh[q] : b;
+    __syncthreads();
+    chosen[rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    if (tid == 0) emit(rd, b);
+  }
+}
+
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
                          float *probs, hipStream_t s) {
   if (T <= 0) return hipSuccess;
@@ -504,7 +576,7 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
     }
 #undef FFMI_SMR
   } else {
-    hipLaunchKernelGGL(softmax_topk_kernel, dim3(T), dim3(256), 0, s, logits, V, k, ids, probs);
+    hipLaunchKernelGGL(softmax_topk_kernel<1024>, dim3(T), dim3(1024), 0, s, logits, V, k, ids, probs);
   }
   return hipGetLastError();
 }

@@ -1,7 +1,7 @@
 """Softmax + argmax / top-k microbenchmark through the C ABI (HIP events):
 the SSM step's top-3 (T = 24) and the verify step's argmax (T = 168) over a
-32000 vocabulary.  V = 31999 takes the 256-thread loop kernel (no 16-B rows),
-for comparison with the register-resident kernel."""
+32000 vocabulary.  V = 31999 / 32001 (no 16-B rows) and 128256 take the
+streaming kernel, for comparison with the register-resident kernel."""
 import os
 import sys
 
@@ -15,7 +15,8 @@ from hip_util import Buf, Timer, f16  # noqa: E402
 
 L = F.lib()
 rng = np.random.default_rng(0)
-for T, V, k in [(24, 32000, 3), (24, 31999, 3), (168, 32000, 1), (8, 32000, 1), (24, 32000, 1)]:
+for T, V, k in [(24, 32000, 3), (24, 31999, 3), (168, 32000, 1), (8, 32000, 1), (24, 32000, 1),
+                (24, 32001, 3), (168, 32001, 1), (24, 128256, 3), (168, 128256, 1)]:
     x = Buf(f16(rng.standard_normal((T, V)) * 3.0))
     ids = Buf.empty((T, k), np.int32)
     pr = Buf.empty((T, k), np.float32)

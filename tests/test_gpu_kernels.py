@@ -263,14 +263,17 @@ def test_softmax_topk_chunked_ties(T, V):
         assert ids.get().tolist() == O.softmax_argmax(logits.astype(np.float32), fp16=1)[0].tolist()
 
 
+@pytest.mark.parametrize("V", [32000, 32001, 128256])
 @pytest.mark.parametrize("nties", [2, 63, 64, 65, 127, 128, 129, 700])
-def test_softmax_topk_candidate_list_capacity(nties):
+def test_softmax_topk_candidate_list_capacity(nties, V):
     """The register kernel puts the candidates' keys in a 128-entry LDS list
     read by one wave (two keys per lane); more candidates fall back to
     workgroup-wide rounds.  Rows with nties equal maxima (and, row 3, half of
-    them 2^-7 lower: fp16 p collapses them) on either side of 64 and 128."""
+    them 2^-7 lower: fp16 p collapses them) on either side of 64 and 128.
+    V = 32001 (rows not 16-B aligned) and 128256 (LLaMA-3) take the streaming
+    kernel, which uses the same list."""
     rng = np.random.default_rng(nties)
-    T, V = 4, 32000
+    T = 4
     logits = f16(rng.standard_normal((T, V)))
     for t in range(T):
         idx = rng.choice(V, nties, replace=False)
