@@ -14,18 +14,6 @@ namespace ffmi {
 __device__ __forceinline__ float h2f_(uint16_t v) { return __half2float(__ushort_as_half(v)); }
 __device__ __forceinline__ uint16_t f2h_(float v) { return __half_as_ushort(__float2half_rn(v)); }
 
-template <typename T>
-__device__ __forceinline__ T block_sum256(T v, T *scratch) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
-  const int wave = threadIdx.x >> 6;
-  if ((threadIdx.x & 63) == 0) scratch[wave] = v;
-  __syncthreads();
-  T r = (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
-  __syncthreads();
-  return r;
-}
-
 template <int NW, typename T>
 __device__ __forceinline__ T block_sum(T v, T *scratch) {
 #pragma unroll
@@ -598,28 +586,19 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
 // all-reduce then acts as an all-gather (x + 0 = x).
 // ---------------------------------------------------------------------------
 template <int TPB>
-__device__ __forceinline__ float block_max(float v, float *sh) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  float m = sh[0];
-#pragma unroll
-  for (int q = 1; q < TPB / 64; ++q) m = fmaxf(m, sh[q]);
-  __syncthreads();
-  return m;
-}
-
-template <int TPB>
 __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict__ logits, int T,
                                                       int Vl, int P, int rank, int k, int phase,
                                                       float *__restrict__ xch, int W,
                                                       int32_t *__restrict__ ids,
                                                       float *__restrict__ probs) {
-  __shared__ double dsh[TPB / 64];
-  __shared__ float fsh[TPB / 64];
-  __shared__ unsigned long long ksh[TPB / 64];
-  const int t = blockIdx.x, tid = threadIdx.x;
+  constexpr int NW = TPB / 64;
+  constexpr int kCand = 128;
+  __shared__ double dsh[NW];
+  __shared__ float fsh[NW];
+  __shared__ unsigned long long ksh[NW];
+  __shared__ unsigned long long cand[kCand];
+  __shared__ unsigned ncand;
+  const int t = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const uint16_t *x = logits + (size_t)t * Vl;
   auto slot = [&](int r) { return xch + ((size_t)r * T + t) * W; };
   if (phase == 3) {  // merge the P*k candidates of the last exchange
@@ -652,7 +631,11 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
   if (phase == 0) {
     float m = -INFINITY;
     for (int i = tid; i < Vl; i += TPB) m = fmaxf(m, h2f_(x[i]));
-    m = block_max<TPB>(m, fsh);
+    m = __ockl_wfred_max_f32(m);
+    if (lane == 0) fsh[wv] = m;
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < NW; ++q) m = fmaxf(m, fsh[q]);
     if (tid < P * W) {
       const int r = tid / W, w = tid % W;
       slot(r)[w] = (r == rank && w == 0) ? m : 0.f;
@@ -666,8 +649,12 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
     //  below only after the whole block has read it)
     double se = 0.0;
     for (int i = tid; i < Vl; i += TPB) se += (double)__expf(h2f_(x[i]) - M);
-    se = block_sum256(se, dsh);
+    se = __ockl_wfred_add_f64(se);
+    if (lane == 0) dsh[wv] = se;
     __syncthreads();
+    se = 0.0;
+#pragma unroll
+    for (int q = 0; q < NW; ++q) se += dsh[q];
     if (tid < P * W) {
       const int r = tid / W, w = tid % W;
       const float hi = (float)se, lo = (float)(se - (double)hi);
@@ -675,42 +662,100 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
     }
     return;
   }
-  // phase 2: global S from the phase-1 records, local top-k candidates
+  // phase 2: global S from the phase-1 records, local top-k candidates --
+  // only logits whose fp16 p can reach the k-th largest local wave maximum's
+  // p are evaluated (the threshold of softmax_topk_reg_kernel), through an
+  // LDS list picked by one wave; k workgroup-wide rounds if it overflows
   double sd = 0.0;
   for (int r = 0; r < P; ++r) {
     const float *q = xch + ((size_t)r * T + t) * W;
     sd += (double)q[1] + (double)q[2];
   }
   const float S = (float)sd;
-  __syncthreads();  // every thread has read the phase-1 records
-  int chosen[4] = {-1, -1, -1, -1};
-  for (int rd = 0; rd < k; ++rd) {
-    unsigned long long best = 0;
-    for (int i = tid; i < Vl; i += TPB) {
-      bool used = false;
-      for (int z = 0; z < rd; ++z) used |= chosen[z] == i;
-      if (used) continue;
-      const uint16_t p = f2h_(__fdiv_rn(expf(h2f_(x[i]) - M), S));
-      const unsigned gi = (unsigned)(rank * Vl + i);
-      const unsigned long long key =
-          ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - gi);
-      best = key > best ? key : best;
+  if (tid == 0) ncand = 0;
+  float wm = -INFINITY;
+  for (int i = tid; i < Vl; i += TPB) wm = fmaxf(wm, h2f_(x[i]));
+  wm = __ockl_wfred_max_f32(wm);
+  if (lane == 0) fsh[wv] = wm;
+  __syncthreads();  // (also: every thread has read the phase-1 records)
+  float L = -INFINITY;
+  {
+    float top[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int q = 0; q < NW; ++q) {
+      float v = fsh[q];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float hi = fmaxf(top[j], v), lo = fminf(top[j], v);
+        top[j] = hi, v = lo;
+      }
     }
 #pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const unsigned long long ot = __shfl_xor(best, o);
-      best = ot > best ? ot : best;
+    for (int j = 0; j < 4; ++j)
+      if (j == k - 1) L = top[j];
+  }
+  float thr = -3.402823466e38f;
+  {
+    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    if (pL > 1) {
+      const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
+      thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
     }
-    if ((tid & 63) == 0) ksh[tid >> 6] = best;
-    __syncthreads();
-    unsigned long long b = ksh[0];
+  }
+  auto key_of = [&](float xv, int i) -> unsigned long long {
+    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    const unsigned gi = (unsigned)(rank * Vl + i);
+    return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - gi);
+  };
+  auto emit = [&](int rd, unsigned long long b) {
+    own[2 * rd] = b ? h2f_((uint16_t)((b >> 32) - 1u)) : 0.f;
+    own[2 * rd + 1] = b ? (float)(0xffffffffu - (unsigned)(b & 0xffffffffu)) : -1.f;
+  };
+  for (int i = tid; i < Vl; i += TPB) {
+    const float xv = h2f_(x[i]);
+    if (xv >= thr) {
+      const unsigned sl = atomicAdd(&ncand, 1u);
+      if (sl < (unsigned)kCand) cand[sl] = key_of(xv, i);
+    }
+  }
+  __syncthreads();
+  const unsigned n = ncand;
+  if (n <= (unsigned)kCand) {
+    if (wv == 0) {  // keys are distinct (they hold the index)
+      unsigned long long a = (unsigned)lane < n ? cand[lane] : 0ull;
+      unsigned long long b = (unsigned)(lane + 64) < n ? cand[lane + 64] : 0ull;
+      for (int rd = 0; rd < k; ++rd) {
+        const unsigned long long best = __ockl_wfred_max_u64(a > b ? a : b);
+        if (lane == 0) emit(rd, best);
+        if (best) {
+          if (a == best) a = 0ull;
+          if (b == best) b = 0ull;
+        }
+      }
+    }
+  } else {
+    int chosen[4] = {-1, -1, -1, -1};
+    for (int rd = 0; rd < k; ++rd) {
+      unsigned long long best = 0;
+      for (int i = tid; i < Vl; i += TPB) {
+        const float xv = h2f_(x[i]);
+        if (xv < thr) continue;
+        bool used = false;
 #pragma unroll
-    for (int q = 1; q < TPB / 64; ++q) b = ksh[q] > b ? ksh[q] : b;
-    __syncthreads();
-    chosen[rd] = b ? (int)(0xffffffffu - (unsigned)(b & 0xffffffffu)) - rank * Vl : -1;
-    if (tid == 0) {
-      own[2 * rd] = b ? h2f_((uint16_t)((b >> 32) - 1u)) : 0.f;
-      own[2 * rd + 1] = b ? (float)(0xffffffffu - (unsigned)(b & 0xffffffffu)) : -1.f;
+        for (int z = 0; z < 4; ++z) used |= (z < rd && chosen[z] == i);
+        if (used) continue;
+        const unsigned long long key = key_of(xv, i);
+        best = key > best ? key : best;
+      }
+      best = __ockl_wfred_max_u64(best);
+      if (lane == 0) ksh[wv] = best;
+      __syncthreads();
+      unsigned long long b = ksh[0];
+#pragma unroll
+      for (int q = 1; q < NW; ++q) b = ksh[q] > b ? ksh[q] : b;
+      __syncthreads();
+      chosen[rd] = b ? (int)(0xffffffffu - (unsigned)(b & 0xffffffffu)) - rank * Vl : -1;
+      if (tid == 0) emit(rd, b);
     }
   }
   if (tid < P * W) {  // zero the other ranks' slots and this slot's unused tail
@@ -725,7 +770,7 @@ hipError_t launch_vshard(const uint16_t *logits, int T, int Vl, int P, int rank,
                          hipStream_t s) {
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4 || P * W > 256 || W < 2 * k || W < 4) return hipErrorInvalidValue;
-  hipLaunchKernelGGL((vshard_kernel<256>), dim3(T), dim3(256), 0, s, logits, T, Vl, P, rank, k,
+  hipLaunchKernelGGL((vshard_kernel<1024>), dim3(T), dim3(1024), 0, s, logits, T, Vl, P, rank, k,
                      phase, xch, W, ids, probs);
   return hipGetLastError();
 }
