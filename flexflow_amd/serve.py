@@ -4,8 +4,9 @@ python/flexflow/serve/serve.py LLM/SSM).  All work happens in the C++
 runtime and HIP kernels; this file only marshals arguments.
 """
 import ctypes
+import os
 from dataclasses import dataclass, field
-from typing import List, Optional
+from typing import List, Optional, Union
 
 from . import ffmi as F
 
@@ -162,6 +163,7 @@ class GenerationResult:
     ssm_decoding_steps: int = 0
     latency_us: float = 0.0
     ttft_us: float = 0.0
+    output_text: str = ""  # tokenizer.decode(output_tokens) when one is registered
 
 
 class RequestManager:
@@ -178,6 +180,8 @@ class RequestManager:
         self.handle = h
         self.guids: List[int] = []
         self._ssms = []
+        self._bos = bos_token_id
+        self.tokenizer = None
 
     def close(self):
         if getattr(self, "handle", None):
@@ -201,7 +205,15 @@ class RequestManager:
         """The text of each output record is tokenizer.decode(tokens), as the
         reference's tokenizer_->Decode (request_manager.cc:786-789).  Any
         object with decode(list[int]) -> str: a `tokenizers.Tokenizer`, an HF
-        tokenizer, or a test double.  BOS/EOS stay as configured at creation."""
+        tokenizer, or a test double; or a path, resolved like the reference's
+        register_tokenizer (request_manager.cc:181-217, tokenizer.json first,
+        then tokenizer.model; flexflow_amd.tokenizer).  A tokenizer with
+        encode(str) also lets register_new_request take text prompts.  BOS/EOS
+        stay as configured at creation."""
+        if isinstance(tokenizer, (str, os.PathLike)):
+            from .tokenizer import load_tokenizer
+            tokenizer = load_tokenizer(os.fspath(tokenizer), self._bos)
+        self.tokenizer = tokenizer
         if tokenizer is None:
             self._detok = None
             F.check(F.lib().ffmi_rm_register_detokenizer(self.handle, None, None), "detok")
@@ -228,8 +240,17 @@ class RequestManager:
         F.check(F.lib().ffmi_rm_register_detokenizer(
             self.handle, ctypes.cast(self._detok, ctypes.c_void_p), None), "detok")
 
-    def register_new_request(self, prompt: List[int], max_length=-1, max_new_tokens=-1,
-                             add_special_tokens=True) -> int:
+    def register_new_request(self, prompt: Union[str, List[int]], max_length=-1,
+                             max_new_tokens=-1, add_special_tokens=True) -> int:
+        """Token ids, or text encoded by the registered tokenizer without
+        special tokens (request_manager.cc:369-373; BOS is prepended by the
+        request manager when add_special_tokens is set)."""
+        if isinstance(prompt, str):
+            if self.tokenizer is None or not hasattr(self.tokenizer, "encode"):
+                raise ValueError("text prompt needs a tokenizer with encode() "
+                                 "(register_tokenizer); the reference asserts "
+                                 "'Tokenizer is null!'")
+            prompt = self.tokenizer.encode(prompt)
         arr = F.int_array(list(prompt))
         g = F.lib().ffmi_rm_register_request(self.handle, arr, len(prompt), max_length,
                                              max_new_tokens, int(add_special_tokens))
@@ -251,9 +272,15 @@ class RequestManager:
         p = F.Profile()
         F.check(L.ffmi_rm_get_profile(self.handle, guid, ctypes.byref(p)), "profile")
         out = list(buf[:n])
+        text = ""
+        if self.tokenizer is not None:
+            try:
+                text = self.tokenizer.decode(out)
+            except Exception:  # a decode-less test double
+                text = ""
         return GenerationResult(guid, out[:p.input_len], out, p.llm_decoding_steps,
                                 p.ssm_decoding_steps, p.finish_us - p.start_us,
-                                p.first_token_us - p.registration_us)
+                                p.first_token_us - p.registration_us, text)
 
     def stats(self) -> F.ServeStats:
         s = F.ServeStats()
