@@ -181,6 +181,7 @@ class RequestManager:
         self.guids: List[int] = []
         self._ssms = []
         self._bos = bos_token_id
+        self.max_sequence_length = max_sequence_length
         self.tokenizer = None
 
     def close(self):
@@ -240,11 +241,22 @@ class RequestManager:
         F.check(F.lib().ffmi_rm_register_detokenizer(
             self.handle, ctypes.cast(self._detok, ctypes.c_void_p), None), "detok")
 
-    def register_new_request(self, prompt: Union[str, List[int]], max_length=-1,
-                             max_new_tokens=-1, add_special_tokens=True) -> int:
+    def register_new_request(self, prompt: Union[str, List[int], None], max_length=-1,
+                             max_new_tokens=-1, add_special_tokens=True,
+                             benchmarking_tokens=-1) -> int:
         """Token ids, or text encoded by the registered tokenizer without
         special tokens (request_manager.cc:369-373; BOS is prepended by the
-        request manager when add_special_tokens is set)."""
+        request manager when add_special_tokens is set).
+
+        benchmarking_tokens >= 0 is the reference's synthetic-prompt mode
+        (:362-369): the prompt is that many copies of token 15 and `prompt` is
+        ignored; it must be below max_sequence_length (the reference asserts).
+        Deviation: max_new_tokens counts from that prompt here, where the
+        reference leaves max_length unset in this mode."""
+        if benchmarking_tokens >= 0:
+            if benchmarking_tokens >= self.max_sequence_length:
+                raise ValueError("Benchmarking tokens exceed max sequence length")
+            prompt = [15] * benchmarking_tokens
         if isinstance(prompt, str):
             if self.tokenizer is None or not hasattr(self.tokenizer, "encode"):
                 raise ValueError("text prompt needs a tokenizer with encode() "

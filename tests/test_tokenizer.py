@@ -107,3 +107,17 @@ def test_text_prompt_without_tokenizer_is_an_error():
     rm = fa.RequestManager(max_requests_per_batch=1, max_tokens_per_batch=16)
     with pytest.raises(ValueError):
         rm.register_new_request("hello")
+
+
+def test_benchmarking_tokens_prompt():
+    """request_manager.cc:358-369: BOS + benchmarking_tokens copies of 15."""
+    V = 997
+    rm = fa.RequestManager(max_requests_per_batch=2, max_tokens_per_batch=16,
+                           max_sequence_length=128)
+    llm = fa.HashModel(V, "inc", max_requests=2, max_seq_len=128)
+    g = rm.register_new_request(None, max_length=40, benchmarking_tokens=20)
+    rm.serve_incr_decoding(llm)
+    r = rm.get_generation_result(g)
+    assert r.input_tokens == [1] + [15] * 20 and len(r.output_tokens) == 40
+    with pytest.raises(ValueError):
+        rm.register_new_request(None, benchmarking_tokens=128)
