@@ -407,6 +407,11 @@ def main():
         with open("/proc/self/maps") as f, open(os.environ["FFMI_DUMP_MAPS"], "w") as g:
             g.write(f.read())
 
+    # every rank has built its models (weights generated or loaded, graphs
+    # not yet) before the first collective: the xGMI all-reduce waits at most
+    # FFMI_PEER_TIMEOUT_S for a peer, and loading skew must not eat into that
+    device_sync()
+    ctrl.barrier()
     for _ in range(args.warmup):
         run_generate(rm, llm, prompts, max_len, spec)
     if args.profile:

@@ -844,6 +844,8 @@ bool comm_has_peer(const ffmi_comm *c, size_t bytes) {
   return c && c->peer && c->peer->attached && bytes <= c->peer->cap;
 }
 int comm_size(const ffmi_comm *c) { return c ? c->nranks : 1; }
+bool comm_peer_attached(const ffmi_comm *c) { return c && c->peer && c->peer->attached; }
+bool comm_has_fallback(const ffmi_comm *c) { return c && (c->comm || c->local); }
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
                                 int ld, int col0, int dtype, hipStream_t s) {
   return peer_run(c, in, out, rows, cols, ld, col0, dtype, s);
@@ -888,8 +890,14 @@ extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, s
   FFMI_CHECK(c && in && out, FFMI_ERR_INVALID);
   if (c->nranks > 1 && c->peer && c->peer->attached && dtype != FFMI_I32) {
     const size_t esz = dtype == FFMI_F16 ? 2 : 4;
-    FFMI_CHECK(count * esz <= c->peer->cap, FFMI_ERR_INVALID);
-    return peer_run(c, in, out, 1, count, count, 0, dtype, (hipStream_t)stream);
+    if (count * esz <= c->peer->cap)
+      return peer_run(c, in, out, 1, count, count, 0, dtype, (hipStream_t)stream);
+    // larger than the exchange buffers: RCCL or the local group takes it
+    if (!c->comm && !c->local) {
+      ffmi_set_last_error("all-reduce larger than the xGMI exchange buffer and no RCCL "
+                          "communicator to fall back to", __FILE__, __LINE__);
+      return FFMI_ERR_INVALID;
+    }
   }
   FFMI_CHECK(c->local || c->comm || c->nranks == 1, FFMI_ERR_INVALID);
   if (c->local && c->nranks > 1)

@@ -150,6 +150,9 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
                        Partials *defer = nullptr, int wpitch = 0);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
+// fp16 Y[T][N] (row-major) of deferred split-K slabs, summed in slab order and
+// rounded once: the value every consumer of the slabs computes (tensor capture)
+hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, hipStream_t s);
 long attn_debug_stamps(long long *dst, long max_waves);
 long gemm_debug_stamps(long long *dst, long max_waves);
 size_t packed_act_bytes(int T, int K);
@@ -215,6 +218,10 @@ ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool reco
 // transport when attached and the message fits its buffers.
 bool comm_has_peer(const ffmi_comm *c, size_t bytes);
 int comm_size(const ffmi_comm *c);
+// the xGMI transport is attached (whatever its capacity)
+bool comm_peer_attached(const ffmi_comm *c);
+// an RCCL communicator or an in-process group takes what the transport cannot
+bool comm_has_fallback(const ffmi_comm *c);
 // sum of every rank's [rows][cols] `in` into `out` (row stride ld, starting
 // at column col0) over the xGMI transport
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,

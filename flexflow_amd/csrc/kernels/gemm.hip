@@ -799,6 +799,21 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   return hipGetLastError();
 }
 
+hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, hipStream_t s) {
+  if (T <= 0 || p.S <= 0) return hipSuccess;
+  if (p.S > 8 || p.NP % 16 || N > p.NP) return hipErrorInvalidValue;
+  const long total = (long)T * ((N + 3) / 4);
+  const unsigned blocks = (unsigned)((total + 255) / 256);
+#define FFMI_PRED(MS)                                                                          \
+  hipLaunchKernelGGL((gemm_reduce_kernel<0, MS>), dim3(blocks), dim3(256), 0, s, p.p, Y, T, N, \
+                     p.NP / 16, p.S, 0)
+  if (p.S <= 2) FFMI_PRED(2);
+  else if (p.S <= 4) FFMI_PRED(4);
+  else FFMI_PRED(8);
+#undef FFMI_PRED
+  return hipGetLastError();
+}
+
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
                        Partials *defer, int wpitch) {

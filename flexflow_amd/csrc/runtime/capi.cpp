@@ -35,6 +35,11 @@ extern "C" long ffmi_model_debug_tensor(ffmi_model *m, int which, int layer, flo
   return m->debug_tensor(which, layer, out, cap);
 }
 
+extern "C" long ffmi_model_debug_width(ffmi_model *m, int which) {
+  if (!m) return -1;
+  return m->debug_width(which);
+}
+
 extern "C" ffmi_status ffmi_set_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FFMI_ERR_NO_DEVICE;
@@ -89,6 +94,12 @@ extern "C" ffmi_status ffmi_rm_register_detokenizer(ffmi_rm *rm, ffmi_detokenize
                                                     void *ctx) {
   if (!rm) return FFMI_ERR_INVALID;
   rm->rm.register_detokenizer(fn, ctx);
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rm_set_old_llama_tokenizer(ffmi_rm *rm, int enable) {
+  if (!rm) return FFMI_ERR_INVALID;
+  rm->rm.set_old_llama_tokenizer(enable != 0);
   return FFMI_OK;
 }
 

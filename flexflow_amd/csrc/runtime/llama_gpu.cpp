@@ -181,42 +181,82 @@ struct LlamaGPU : public ffmi_model {
   }
 
   // ---- tensor capture (--inference-debugging, operator.h:271-360) ----
+  // kind k (FFMI_DBG_*) keeps [dbg_layers(k)][Tm][dbg_width(k)] fp16 values of
+  // the last eager step; GEMM inputs are stored in their packed tile layout
+  // and unpacked on readout
+  static constexpr int kDbgKinds = 10;
   int dbg = 0;
-  uint16_t *dbg_buf = nullptr;  // [num_layers + 1][Tm][H] fp16 (last slot maybe packed)
+  uint16_t *dbg_buf = nullptr;
+  size_t dbg_off[kDbgKinds] = {};
   int dbg_T = -1;
-  bool dbg_final_packed = false;
+  long debug_width(int k) const override {
+    switch (k) {
+      case FFMI_DBG_LOGITS: return Vl;
+      case FFMI_DBG_QKV: return 3L * Hl;
+      case FFMI_DBG_ATTN_OUT: return Hl;
+      case FFMI_DBG_MLP_ACT: return Fl;
+      case FFMI_DBG_HIDDEN: case FFMI_DBG_ATTN_NORM: case FFMI_DBG_O_PROJ:
+      case FFMI_DBG_FFN_NORM: case FFMI_DBG_DOWN: case FFMI_DBG_EMBED: return c.hidden;
+    }
+    return -1;
+  }
+  int dbg_layers(int k) const {
+    return k == FFMI_DBG_LOGITS ? 0 : k == FFMI_DBG_EMBED ? 1
+                                    : k == FFMI_DBG_HIDDEN ? c.num_layers + 1 : c.num_layers;
+  }
+  // stored in the packed activation-tile layout (a GEMM input written so)
+  bool dbg_is_packed(int k, int layer) const {
+    if (!packed) return false;
+    return k == FFMI_DBG_ATTN_NORM || k == FFMI_DBG_FFN_NORM || k == FFMI_DBG_ATTN_OUT ||
+           k == FFMI_DBG_MLP_ACT || (k == FFMI_DBG_HIDDEN && layer == c.num_layers);
+  }
+  size_t dbg_tm() const { return (size_t)((o.max_tokens + 15) & ~15); }
   ffmi_status set_debug(int enable) override {
     if (enable && !dbg_buf) {
-      const size_t Tm = (size_t)((o.max_tokens + 15) & ~15);
-      if (alloc(&dbg_buf, (size_t)(c.num_layers + 1) * Tm * c.hidden) != FFMI_OK)
-        return FFMI_ERR_OOM;
+      size_t total = 0;
+      for (int k = 0; k < kDbgKinds; ++k) {
+        dbg_off[k] = total;
+        total += (size_t)dbg_layers(k) * dbg_tm() * std::max(0L, debug_width(k));
+      }
+      if (alloc(&dbg_buf, total) != FFMI_OK) return FFMI_ERR_OOM;
     }
     dbg = enable ? 1 : 0;
     dbg_T = -1;
     return FFMI_OK;
   }
-  uint16_t *dbg_slot(int l) const {
-    const size_t Tm = (size_t)((o.max_tokens + 15) & ~15);
-    return dbg_buf + (size_t)l * Tm * c.hidden;
+  uint16_t *dbg_slot(int k, int l) const {
+    return dbg_buf + dbg_off[k] + (size_t)l * dbg_tm() * debug_width(k);
+  }
+  // capture src ([T][width], or packed tiles covering whole 16-row groups)
+  ffmi_status dbg_copy(int k, int l, const uint16_t *src, int T) {
+    const size_t rows = dbg_is_packed(k, l) ? (size_t)((T + 15) & ~15) : (size_t)T;
+    FFMI_HIP(hipMemcpyAsync(dbg_slot(k, l), src, rows * debug_width(k) * 2,
+                            hipMemcpyDeviceToDevice, stream));
+    return FFMI_OK;
+  }
+  // capture a GEMM output that is either written (Y) or left as split-K slabs
+  ffmi_status dbg_gemm_out(int k, int l, const uint16_t *Y, const ffmi::Partials &p, int T) {
+    if (p.S > 0) {
+      FFMI_HIP(ffmi::launch_partials_reduce(p, dbg_slot(k, l), T, (int)debug_width(k), stream));
+      return FFMI_OK;
+    }
+    return dbg_copy(k, l, Y, T);
   }
   long debug_tensor(int which, int layer, float *out, long cap) override {
     if (dbg_T < 0 || (stream && hipStreamSynchronize(stream) != hipSuccess)) return -1;
-    const int T = dbg_T, H = c.hidden;
-    const int width = which == FFMI_DBG_LOGITS ? Vl : H;  // (this rank's vocab shard)
-    if ((which != FFMI_DBG_LOGITS && which != FFMI_DBG_HIDDEN) ||
-        (which == FFMI_DBG_HIDDEN && (layer < 0 || layer > c.num_layers)) ||
-        cap < (long)T * width)
-      return -1;
-    std::vector<uint16_t> h16((size_t)T * width);
-    const uint16_t *src = which == FFMI_DBG_LOGITS ? logits : dbg_slot(layer);
-    const bool pk = which == FFMI_DBG_HIDDEN && layer == c.num_layers && dbg_final_packed;
-    // a packed slot covers whole 16-row tiles
-    const size_t n = pk ? (size_t)((T + 15) & ~15) * width : (size_t)T * width;
+    if (which < 0 || which >= kDbgKinds) return -1;
+    const int T = dbg_T;
+    const long width = debug_width(which);
+    if (which != FFMI_DBG_LOGITS && (layer < 0 || layer >= dbg_layers(which))) return -1;
+    if (cap < (long)T * width) return -1;
+    const uint16_t *src = which == FFMI_DBG_LOGITS ? logits : dbg_slot(which, layer);
+    const bool pk = which != FFMI_DBG_LOGITS && dbg_is_packed(which, layer);
+    const size_t n = (size_t)(pk ? (T + 15) & ~15 : T) * width;
     std::vector<uint16_t> raw(n);
     if (hipMemcpy(raw.data(), src, n * 2, hipMemcpyDeviceToHost) != hipSuccess) return -1;
     for (int t = 0; t < T; ++t)
-      for (int j = 0; j < width; ++j) {
-        const uint16_t b = raw[pk ? act_packed_off(t, j, width) : (size_t)t * width + j];
+      for (long j = 0; j < width; ++j) {
+        const uint16_t b = raw[pk ? act_packed_off(t, (int)j, (int)width) : (size_t)t * width + j];
         _Float16 v;
         memcpy(&v, &b, 2);
         out[(size_t)t * width + j] = (float)v;
@@ -339,6 +379,14 @@ struct LlamaGPU : public ffmi_model {
     if (Vl != V) TRY(alloc(&xch, (ffmi_vocab_shard_scratch_bytes(P, Tm) + 3) / 4));
     TRY(alloc(&ids_d, (size_t)Tm * 4 * 2));  // [ids | probs] of a step, one D2H copy
     peer = P > 1 && ffmi::comm_has_peer(o.comm, (size_t)Tm * H * 2);
+    // an attached transport too small for this model's largest [Tm][H]
+    // all-reduce needs RCCL (or the local group) for those steps: refuse at
+    // creation rather than failing mid-serve
+    if (P > 1 && !peer && ffmi::comm_peer_attached(o.comm) && !ffmi::comm_has_fallback(o.comm)) {
+      ffmi_set_last_error("xGMI exchange buffer smaller than max_tokens x hidden fp16 and no "
+                          "RCCL communicator", __FILE__, __LINE__);
+      return FFMI_ERR_INVALID;
+    }
     if (peer) {
       tp_chunks = 2;
       if (const char *e = getenv("FFMI_TP_OVERLAP")) tp_chunks = atoi(e) ? 2 : 1;
@@ -600,18 +648,22 @@ struct LlamaGPU : public ffmi_model {
                                     l == 0 ? ffmi::Partials() : down_part,
                                     l == 0 ? batch->dev : nullptr));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
-      if (dbg && l > 0)  // residual stream after layer l-1
-        FFMI_HIP(hipMemcpyAsync(dbg_slot(l - 1), res, (size_t)T * H * 2, hipMemcpyDeviceToDevice,
-                                stream));
+      if (dbg) {
+        // residual stream after layer l-1 (layer 0: the embedding rows)
+        TRY(dbg_copy(l == 0 ? FFMI_DBG_EMBED : FFMI_DBG_HIDDEN, l == 0 ? 0 : l - 1, res, T));
+        TRY(dbg_copy(FFMI_DBG_ATTN_NORM, l, h, T));
+      }
       pr = prof_begin(on);
       ffmi::Partials qkv_part;
       FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
                                  &qkv_part));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
+      if (dbg) TRY(dbg_gemm_out(FFMI_DBG_QKV, l, qkv, qkv_part, T));
       pr = prof_begin(on);
       TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s,
                              mode == FFMI_MODEL_TREE ? tree_parity : -1));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
+      if (dbg) TRY(dbg_copy(FFMI_DBG_ATTN_OUT, l, att, T));
       ffmi::Partials o_part;
       if (o.tp_size == 1) {
         pr = prof_begin(on);
@@ -623,14 +675,17 @@ struct LlamaGPU : public ffmi_model {
         TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
       }
+      if (dbg) TRY(dbg_gemm_out(FFMI_DBG_O_PROJ, l, proj, o_part, T));
       pr = prof_begin(on);
       FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
                                     o_part));
       prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+      if (dbg) TRY(dbg_copy(FFMI_DBG_FFN_NORM, l, h, T));
       pr = prof_begin(on);
       const int YP = packed ? FFMI_Y_PACKED : 0;
       TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
+      if (dbg) TRY(dbg_copy(FFMI_DBG_MLP_ACT, l, mlp, T));
       if (o.tp_size == 1) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
@@ -641,6 +696,7 @@ struct LlamaGPU : public ffmi_model {
         TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
       }
+      if (dbg) TRY(dbg_gemm_out(FFMI_DBG_DOWN, l, proj, down_part, T));
     }
     const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
     pr = prof_begin(ptail);
@@ -648,12 +704,8 @@ struct LlamaGPU : public ffmi_model {
                                   down_part));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
     if (dbg) {
-      FFMI_HIP(hipMemcpyAsync(dbg_slot(c.num_layers - 1), res, (size_t)T * H * 2,
-                              hipMemcpyDeviceToDevice, stream));
-      FFMI_HIP(hipMemcpyAsync(dbg_slot(c.num_layers), h,
-                              (size_t)(packed ? (T + 15) & ~15 : T) * H * 2,
-                              hipMemcpyDeviceToDevice, stream));
-      dbg_final_packed = packed;
+      TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers - 1, res, T));
+      TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers, h, T));
       dbg_T = T;
     }
     pr = prof_begin(ptail);

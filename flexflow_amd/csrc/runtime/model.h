@@ -68,6 +68,10 @@ struct ffmi_model {
     (void)cap;
     return -1;
   }
+  virtual long debug_width(int which) const {
+    (void)which;
+    return -1;
+  }
 };
 
 namespace ffmi {

@@ -143,6 +143,14 @@ std::string RequestManager::decode(const std::vector<int> &ids) const {
   return out;
 }
 
+std::string RequestManager::decode_request(const Request &request) const {
+  std::string text = decode(request.tokens);
+  if (detok && old_llama_tokenizer && request.add_special_tokens && !request.tokens.empty() &&
+      request.tokens[0] == bos_token_id)
+    text = "<s> " + text;
+  return text;
+}
+
 // The reference's per-request output record, appended on completion:
 // incremental decoding request_manager.cc:813-840 ("[Profile] guid(..)
 // llm_decoding_steps(..) latency(..) ttft(..)"), SpecInfer :1303-1330 (no
@@ -163,7 +171,7 @@ void RequestManager::write_output_record(const Request &request, bool spec) cons
   for (size_t i = 0; i < request.tokens.size(); ++i)
     fprintf(f, i + 1 < request.tokens.size() ? "%d," : "%d", request.tokens[i]);
   fputc('\n', f);
-  const std::string text = decode(request.tokens);
+  const std::string text = decode_request(request);
   fwrite(text.data(), 1, text.size(), f);
   fclose(f);
 }

@@ -83,6 +83,11 @@ class RequestManager {
   typedef int (*Detokenizer)(const int *ids, int n, char *buf, int cap, void *ctx);
   void register_detokenizer(Detokenizer fn, void *ctx) { detok = fn, detok_ctx = ctx; }
   std::string decode(const std::vector<int> &ids) const;
+  // the text of a completed request: decode(tokens), with the "<s> " prefix
+  // of the old LLaMA tokenizer for requests that asked for special tokens
+  // (request_manager.cc:776-781)
+  std::string decode_request(const Request &request) const;
+  void set_old_llama_tokenizer(bool v) { old_llama_tokenizer = v; }
   void set_verbose(bool v) { verbose = v; }
 
   RequestGuid register_new_request(const std::vector<int> &prompt, int max_length,
@@ -158,6 +163,7 @@ class RequestManager {
   std::string output_filepath;
   Detokenizer detok = nullptr;
   void *detok_ctx = nullptr;
+  bool old_llama_tokenizer = false;
 
   std::deque<Request> pending_infr_request_queue;
   std::map<RequestGuid, Request> all_requests;

@@ -21,7 +21,10 @@ STATUS = {0: "ok", 1: "invalid argument", 2: "hip error", 3: "rccl error", 4: "o
           5: "unsupported", 6: "no gfx950 device"}
 ATTN_INC, ATTN_SPEC, ATTN_TREE = 0, 1, 2
 MODEL_INC, MODEL_BEAM, MODEL_TREE = 0, 1, 2
-DBG_HIDDEN, DBG_LOGITS = 0, 1  # ffmi_model_debug_tensor kinds
+# ffmi_model_debug_tensor kinds (include/ffmi.h FFMI_DBG_*)
+DBG_KINDS = {"hidden": 0, "logits": 1, "attn_norm": 2, "qkv": 3, "attn_out": 4, "o_proj": 5,
+             "ffn_norm": 6, "mlp_act": 7, "down": 8, "embed": 9}
+DBG_HIDDEN, DBG_LOGITS = DBG_KINDS["hidden"], DBG_KINDS["logits"]
 EPI_NONE, EPI_SILU_MUL = 0, 1
 X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
 Y_PACKED = 0x20  # FFMI_Y_PACKED
@@ -158,12 +161,14 @@ SIGNATURES = {
     "ffmi_model_op_stats": (c_int, [c_void_p, ctypes.POINTER(OpStat), c_int]),
     "ffmi_model_set_debug": (c_int, [c_void_p, c_int]),
     "ffmi_model_debug_tensor": (ctypes.c_long, [c_void_p, c_int, c_int, c_void_p, ctypes.c_long]),
+    "ffmi_model_debug_width": (ctypes.c_long, [c_void_p, c_int]),
     "ffmi_set_device": (c_int, [c_int]),
     "ffmi_rm_create": (c_int, [ctypes.POINTER(RMConfig), ctypes.POINTER(c_void_p)]),
     "ffmi_rm_destroy": (None, [c_void_p]),
     "ffmi_rm_register_ssm": (c_int, [c_void_p, c_void_p]),
     "ffmi_rm_register_output_filepath": (c_int, [c_void_p, ctypes.c_char_p]),
     "ffmi_rm_register_detokenizer": (c_int, [c_void_p, c_void_p, c_void_p]),
+    "ffmi_rm_set_old_llama_tokenizer": (c_int, [c_void_p, c_int]),
     "ffmi_rm_register_request": (c_int64, [c_void_p, ctypes.POINTER(c_int), c_int, c_int, c_int,
                                            c_int]),
     "ffmi_rm_serve_incr_decoding": (c_int, [c_void_p, c_void_p]),

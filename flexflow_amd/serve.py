@@ -50,11 +50,17 @@ class Model:
         F.check(F.lib().ffmi_model_set_debug(self.handle, int(enable)), "set_debug")
 
     def debug_tensor(self, which: str, layer: int = 0):
-        """'hidden' (layer l < num_layers: residual stream after layer l;
-        layer == num_layers: final norm output) or 'logits', as fp32 [T][width]."""
+        """A captured tensor of the last step as fp32 [T][width]:
+        'hidden' (layer l < num_layers: residual stream after layer l;
+        layer == num_layers: final norm output), 'logits' (this rank's vocab
+        shard under a vocab-sharded lm_head), or an op of layer l: 'embed',
+        'attn_norm', 'qkv', 'attn_out', 'o_proj', 'ffn_norm', 'mlp_act',
+        'down' (include/ffmi.h FFMI_DBG_*; shard widths under TP)."""
         import numpy as np
-        width = self.config["vocab_size"] if which == "logits" else self.config["hidden"]
-        kind = F.DBG_LOGITS if which == "logits" else F.DBG_HIDDEN
+        kind = F.DBG_KINDS[which]
+        width = F.lib().ffmi_model_debug_width(self.handle, kind)
+        if width <= 0:
+            raise F.FFMIError(f"debug_tensor({which}): no such tensor")
         buf = np.empty(1024 * width, np.float32)
         T = F.lib().ffmi_model_debug_tensor(self.handle, kind, layer,
                                             buf.ctypes.data_as(ctypes.c_void_p), buf.size)
@@ -183,6 +189,7 @@ class RequestManager:
         self._bos = bos_token_id
         self.max_sequence_length = max_sequence_length
         self.tokenizer = None
+        self._add_special = {}
 
     def close(self):
         if getattr(self, "handle", None):
@@ -215,6 +222,8 @@ class RequestManager:
             from .tokenizer import load_tokenizer
             tokenizer = load_tokenizer(os.fspath(tokenizer), self._bos)
         self.tokenizer = tokenizer
+        F.check(F.lib().ffmi_rm_set_old_llama_tokenizer(
+            self.handle, int(bool(getattr(tokenizer, "old_llama_tokenizer", False)))), "tokenizer")
         if tokenizer is None:
             self._detok = None
             F.check(F.lib().ffmi_rm_register_detokenizer(self.handle, None, None), "detok")
@@ -268,6 +277,7 @@ class RequestManager:
                                              max_new_tokens, int(add_special_tokens))
         if g > 0:
             self.guids.append(g)
+            self._add_special[g] = bool(add_special_tokens)
         return g
 
     def serve_incr_decoding(self, llm: Model):
@@ -290,6 +300,10 @@ class RequestManager:
                 text = self.tokenizer.decode(out)
             except Exception:  # a decode-less test double
                 text = ""
+            # the old LLaMA tokenizer's "<s> " prefix (request_manager.cc:776-781)
+            if (getattr(self.tokenizer, "old_llama_tokenizer", False) and
+                    self._add_special.get(guid, True) and out and out[0] == self._bos):
+                text = "<s> " + text
         return GenerationResult(guid, out[:p.input_len], out, p.llm_decoding_steps,
                                 p.ssm_decoding_steps, p.finish_us - p.start_us,
                                 p.first_token_us - p.registration_us, text)

@@ -15,8 +15,10 @@ Text semantics kept from the reference:
 - on completion a trailing EOS is dropped before decoding (:772-775, in the
   C++ request manager here);
 - SentencePiece drops BOS when decoding, so the reference prefixes "<s> " to
-  the text when the old LLaMA tokenizer is in use and the sequence starts
-  with BOS (:776-781).
+  the text when the old LLaMA tokenizer is in use, the request was registered
+  with add_special_tokens and its tokens start with BOS (:776-781).  That rule
+  belongs to the request manager (it knows add_special_tokens per request):
+  RequestManager applies it, decode() here is the bare Decode.
 Whether tokenizers-cpp's Encode/Decode skip special tokens is not visible in
 the reference tree (empty submodule): the HF path here encodes without and
 decodes with special tokens, and that choice is parity-unpinned.
@@ -60,10 +62,7 @@ class LlamaTokenizer:
     def decode(self, ids: List[int]) -> str:
         ids = list(ids)
         if self._sp is not None:
-            text = self._sp.decode(ids)
-            if ids and ids[0] == self.bos_token_id:
-                text = "<s> " + text
-            return text
+            return self._sp.decode(ids)
         return self._hf.decode(ids, skip_special_tokens=False)
 
 

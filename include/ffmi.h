@@ -345,14 +345,36 @@ int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap);
  *   FFMI_DBG_HIDDEN, layer l in [0, num_layers): the residual stream after
  *     decoder layer l (HF hidden_states[l + 1]); layer == num_layers: the
  *     final RMSNorm output (HF's last hidden state);
- *   FFMI_DBG_LOGITS: the lm_head output [T][vocab] (before softmax).
- * ffmi_model_debug_tensor copies one as fp32 rows [T][width] into `out`
- * (capacity `cap` floats) and returns T, or -1 (nothing captured / bad
- * argument / too small).  Replicated under TP: every rank returns the same. */
+ *   FFMI_DBG_LOGITS: the lm_head output [T][V_l] (before softmax; V_l = this
+ *     rank's vocab shard when the lm_head is vocab-sharded, else vocab);
+ * and per op of decoder layer l, the tensors the reference's alignment test
+ * compares (inference_alignment_test.py:20-370: embedding, the two norms,
+ * the QKV projection with its shard re-assembly, attention output, MLP):
+ *   FFMI_DBG_EMBED      [T][H]     embedding rows (layer 0 only)
+ *   FFMI_DBG_ATTN_NORM  [T][H]     input_layernorm output
+ *   FFMI_DBG_QKV        [T][3*H_l] qkv_proj output before RoPE, [Q_s|K_s|V_s]
+ *   FFMI_DBG_ATTN_OUT   [T][H_l]   attention output (o_proj input)
+ *   FFMI_DBG_O_PROJ     [T][H]     o_proj output (after the all-reduce)
+ *   FFMI_DBG_FFN_NORM   [T][H]     post_attention_layernorm output
+ *   FFMI_DBG_MLP_ACT    [T][F_l]   SiLU(gate) * up (down_proj input)
+ *   FFMI_DBG_DOWN       [T][H]     down_proj output (after the all-reduce)
+ * H_l / F_l are this rank's shard widths.  ffmi_model_debug_tensor copies one
+ * as fp32 rows [T][width] into `out` (capacity `cap` floats) and returns T,
+ * or -1 (nothing captured / bad argument / too small);
+ * ffmi_model_debug_width returns the width (or -1). */
 #define FFMI_DBG_HIDDEN 0
 #define FFMI_DBG_LOGITS 1
+#define FFMI_DBG_ATTN_NORM 2
+#define FFMI_DBG_QKV 3
+#define FFMI_DBG_ATTN_OUT 4
+#define FFMI_DBG_O_PROJ 5
+#define FFMI_DBG_FFN_NORM 6
+#define FFMI_DBG_MLP_ACT 7
+#define FFMI_DBG_DOWN 8
+#define FFMI_DBG_EMBED 9
 ffmi_status ffmi_model_set_debug(ffmi_model *m, int enable);
 long ffmi_model_debug_tensor(ffmi_model *m, int which, int layer, float *out, long cap);
+long ffmi_model_debug_width(ffmi_model *m, int which);
 /* select the HIP device of the calling thread (one process per GPU) */
 ffmi_status ffmi_set_device(int device);
 
@@ -383,6 +405,12 @@ ffmi_status ffmi_rm_register_output_filepath(ffmi_rm *rm, const char *path);
  * NULL fn: empty text (no tokenizer). */
 typedef int (*ffmi_detokenize_fn)(const int *ids, int n, char *buf, int cap, void *ctx);
 ffmi_status ffmi_rm_register_detokenizer(ffmi_rm *rm, ffmi_detokenize_fn fn, void *ctx);
+/* The tokenizer is the old LLaMA SentencePiece model (the reference's
+ * old_llama_tokenizer, request_manager.cc:200-211): SentencePiece drops BOS
+ * when decoding, so the text of a request registered with
+ * add_special_tokens whose tokens start with BOS gets a "<s> " prefix
+ * (:776-781). */
+ffmi_status ffmi_rm_set_old_llama_tokenizer(ffmi_rm *rm, int enable);
 /* Request: prompt token ids (BOS is prepended when bos_token_id >= 0 and
  * add_special_tokens), max_length / max_new_tokens as in Request
  * (request_manager.cc:334-441).  Returns guid (> 0) or 0 on rejection. */

@@ -5,12 +5,15 @@
 // hugolatendresse/FlexFlow @ 2025-01-17.
 #include "oracle.h"
 
+#include <immintrin.h>
 #include <math.h>
 #include <omp.h>
 #include <string.h>
 
 #include <algorithm>
 #include <string>
+#include <memory>
+#include <utility>
 #include <vector>
 
 // ----------------------------------------------------------------------------
@@ -132,15 +135,79 @@ static inline float dot_ref16(const float *a, const float *b, int K) {
   return acc;
 }
 
+// Summation-order variant of the fp32 dot (orc_set_dot_variant): 0 = dot8
+// (the oracle's order), 1 = dot16 (16 interleaved partial sums, lanes j and
+// j + 8 added before dot8's pairwise combine).  Both are exact fp32
+// restatements of the same sum in different orders; running the model in
+// both measures the drift that ANY change of fp32 summation order produces
+// (the noise floor a GPU/CPU comparison sits on), tests only.
+static int g_dot_variant = 0;
+extern "C" void orc_set_dot_variant(int v) { g_dot_variant = v == 1 ? 1 : 0; }
+
+// dot8 of R rows of X against one weight row at once: R independent
+// accumulator chains (the single chain of dot8 is add-latency bound), each
+// with exactly dot8's summation order, so the results are bit-identical.
+template <int R>
+static inline void dot8_rows(const float *const *x, const float *w, int K, float *out) {
+  __m256 acc[R], acc2[R];
+  for (int r = 0; r < R; ++r) acc[r] = acc2[r] = _mm256_setzero_ps();
+  int k = 0;
+  if (g_dot_variant == 1) {
+    for (; k + 16 <= K; k += 16) {
+      const __m256 wv = _mm256_loadu_ps(w + k), wv2 = _mm256_loadu_ps(w + k + 8);
+      for (int r = 0; r < R; ++r) {
+        acc[r] = _mm256_add_ps(acc[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k), wv));
+        acc2[r] = _mm256_add_ps(acc2[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k + 8), wv2));
+      }
+    }
+    for (int r = 0; r < R; ++r) acc[r] = _mm256_add_ps(acc[r], acc2[r]);
+  }
+  for (; k + 8 <= K; k += 8) {
+    const __m256 wv = _mm256_loadu_ps(w + k);
+    for (int r = 0; r < R; ++r)
+      acc[r] = _mm256_add_ps(acc[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k), wv));
+  }
+  for (int r = 0; r < R; ++r) {
+    float s[8];
+    _mm256_storeu_ps(s, acc[r]);
+    for (int kk = k; kk < K; ++kk) s[kk & 7] += x[r][kk] * w[kk];
+    out[r] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  }
+}
+
 // linear_kernels.cu:450-582 (cublasGemmEx OP_T/OP_N, out = in . W^T).
 extern "C" void orc_linear(const float *X, const float *W, float *Y, int T,
                            int N, int K, int fp16) {
+  if (fp16 == ORC_REF16) {
 #pragma omp parallel for schedule(static)
-  for (int n = 0; n < N; ++n) {
-    const float *w = W + (size_t)n * K;
-    for (int t = 0; t < T; ++t)
-      Y[(size_t)t * N + n] = fp16 == ORC_REF16 ? dot_ref16(X + (size_t)t * K, w, K)
-                                               : R(dot8(X + (size_t)t * K, w, K), fp16);
+    for (int n = 0; n < N; ++n)
+      for (int t = 0; t < T; ++t)
+        Y[(size_t)t * N + n] = dot_ref16(X + (size_t)t * K, W + (size_t)n * K, K);
+    return;
+  }
+  // blocks of 8 weight rows x 4 activation rows: both stay in L2 while the
+  // block is computed (every element still gets its own dot8)
+  constexpr int NB = 8;
+#pragma omp parallel for schedule(static)
+  for (int n0 = 0; n0 < N; n0 += NB) {
+    const int n1 = std::min(N, n0 + NB);
+    float o[4];
+    int t = 0;
+    for (; t + 4 <= T; t += 4) {
+      const float *x[4] = {X + (size_t)t * K, X + (size_t)(t + 1) * K, X + (size_t)(t + 2) * K,
+                           X + (size_t)(t + 3) * K};
+      for (int n = n0; n < n1; ++n) {
+        dot8_rows<4>(x, W + (size_t)n * K, K, o);
+        for (int r = 0; r < 4; ++r) Y[(size_t)(t + r) * N + n] = R(o[r], fp16);
+      }
+    }
+    for (; t < T; ++t) {
+      const float *x[1] = {X + (size_t)t * K};
+      for (int n = n0; n < n1; ++n) {
+        dot8_rows<1>(x, W + (size_t)n * K, K, o);
+        Y[(size_t)t * N + n] = R(o[0], fp16);
+      }
+    }
   }
 }
 
@@ -363,27 +430,64 @@ extern "C" void orc_softmax_topk(const float *logits, int T, int V, int k,
 // (embedding -> [rms | residual_rms] -> qkv -> IncMHA -> o -> residual_rms
 //  -> gate/up -> silu_mul -> down) x L -> residual_rms "norm" -> lm_head.
 // ----------------------------------------------------------------------------
+// std::vector whose resize() leaves floats uninitialised: the weights are
+// generated in parallel right after, and a serial zero-fill of 27 GB (LLaMA-7B
+// in fp32) took longer than generating them
+template <class T>
+struct DefaultInitAlloc : std::allocator<T> {
+  template <class U>
+  struct rebind {
+    using other = DefaultInitAlloc<U>;
+  };
+  DefaultInitAlloc() = default;
+  template <class U>
+  DefaultInitAlloc(const DefaultInitAlloc<U> &) {}
+  template <class U>
+  void construct(U *p) noexcept {
+    ::new ((void *)p) U;
+  }
+  template <class U, class... A>
+  void construct(U *p, A &&...a) {
+    ::new ((void *)p) U(std::forward<A>(a)...);
+  }
+};
+using fvec = std::vector<float, DefaultInitAlloc<float>>;
+
 struct orc_model {
   orc_config c;
   int fp16;
   int max_requests, max_seq;
   int d;
-  std::vector<float> emb, lm, final_norm;
+  fvec emb, lm, final_norm;
   struct Layer {
-    std::vector<float> in_norm, post_norm, wq, wk, wv, wo, wg, wu, wd;
+    fvec in_norm, post_norm, wq, wk, wv, wo, wg, wu, wd;
   };
   std::vector<Layer> layers;
   std::vector<float> kc, vc;  // [req][layer][pos][H]
   std::vector<float> rope;    // [max_seq][d/2][2]
   std::vector<std::vector<float>> hidden;  // debug: per-layer output of last call
+  // per-op tensors of the last orc_model_forward_ex call, by FFMI_DBG_* kind
+  // (include/ffmi.h: 2 attn_norm, 3 qkv (pre-RoPE [Q|K|V]), 4 attn_out,
+  // 5 o_proj, 6 ffn_norm, 7 mlp_act, 8 down, 9 embed), [layer][T * width]
+  std::vector<std::vector<float>> ops[10];
+  int ops_T = 0;
 };
 
-static void gen(std::vector<float> &dst, const std::string &name, uint64_t seed,
+static void keep_op(orc_model *m, int kind, int layer, const float *src, size_t n) {
+  auto &v = m->ops[kind];
+  if ((int)v.size() <= layer) v.resize(layer + 1);
+  v[layer].assign(src, src + n);
+}
+
+static void gen(fvec &dst, const std::string &name, uint64_t seed,
                 int kind, size_t n, int fp16) {
   dst.resize(n);
   orc_gen_weight(name.c_str(), seed, kind, n, dst.data());
-  if (fp16)
-    for (auto &v : dst) v = orc_round16(v);
+  if (fp16) {
+    float *p = dst.data();
+#pragma omp parallel for schedule(static)
+    for (long i = 0; i < (long)n; ++i) p[i] = orc_round16(p[i]);
+  }
 }
 
 extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
@@ -430,7 +534,7 @@ extern "C" void orc_model_reset(orc_model *m, int req) {
 
 extern "C" long orc_model_weight(orc_model *m, const char *name, float *out) {
   std::string n(name);
-  const std::vector<float> *src = nullptr;
+  const fvec *src = nullptr;
   if (n == "model.embed_tokens.weight") src = &m->emb;
   else if (n == "lm_head.weight") src = &m->lm;
   else if (n == "model.norm.weight") src = &m->final_norm;
@@ -477,6 +581,8 @@ extern "C" int orc_model_forward_ex(orc_model *m, int req, const int *tokens, in
   std::vector<float> g((size_t)T * F), u((size_t)T * F), a((size_t)T * F);
   for (int t = 0; t < T; ++t)
     memcpy(&x[(size_t)t * H], &m->emb[(size_t)tokens[t] * H], H * sizeof(float));
+  m->ops_T = T;
+  keep_op(m, 9, 0, x.data(), x.size());
   const float scale = 1.0f / sqrtf((float)d);
   for (int l = 0; l < c.num_layers; ++l) {
     auto &L = m->layers[l];
@@ -489,9 +595,19 @@ extern "C" int orc_model_forward_ex(orc_model *m, int req, const int *tokens, in
                            h.data(), T, H, c.rms_eps, fp16);
       res.swap(r2);
     }
+    keep_op(m, 2, l, h.data(), h.size());
     orc_linear(h.data(), L.wq.data(), q.data(), T, H, H, fp16);
     orc_linear(h.data(), L.wk.data(), k.data(), T, H, H, fp16);
     orc_linear(h.data(), L.wv.data(), v.data(), T, H, H, fp16);
+    {
+      std::vector<float> qkv3((size_t)T * 3 * H);
+      for (int t = 0; t < T; ++t) {
+        memcpy(&qkv3[(size_t)t * 3 * H], &q[(size_t)t * H], H * sizeof(float));
+        memcpy(&qkv3[(size_t)t * 3 * H + H], &k[(size_t)t * H], H * sizeof(float));
+        memcpy(&qkv3[(size_t)t * 3 * H + 2 * H], &v[(size_t)t * H], H * sizeof(float));
+      }
+      keep_op(m, 3, l, qkv3.data(), qkv3.size());
+    }
     float *kc = &m->kc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
     float *vc = &m->vc[(((size_t)req * c.num_layers + l) * m->max_seq) * H];
     for (int t = 0; t < T; ++t) {
@@ -537,17 +653,22 @@ extern "C" int orc_model_forward_ex(orc_model *m, int req, const int *tokens, in
         }
       }
     }
+    keep_op(m, 4, l, att.data(), att.size());
     orc_linear(att.data(), L.wo.data(), o.data(), T, H, H, fp16);
+    keep_op(m, 5, l, o.data(), o.size());
     {
       std::vector<float> r2((size_t)T * H);
       orc_residual_rmsnorm(res.data(), o.data(), L.post_norm.data(), r2.data(),
                            h.data(), T, H, c.rms_eps, fp16);
       res.swap(r2);
     }
+    keep_op(m, 6, l, h.data(), h.size());
     orc_linear(h.data(), L.wg.data(), g.data(), T, F, H, fp16);
     orc_linear(h.data(), L.wu.data(), u.data(), T, F, H, fp16);
     orc_silu_mul(g.data(), u.data(), a.data(), (size_t)T * F, fp16);
+    keep_op(m, 7, l, a.data(), a.size());
     orc_linear(a.data(), L.wd.data(), mlp.data(), T, H, F, fp16);
+    keep_op(m, 8, l, mlp.data(), mlp.size());
     // debug: residual stream entering the next layer (= res + mlp)
     auto &dbg = m->hidden[l];
     dbg.resize((size_t)T * H);
@@ -636,6 +757,13 @@ extern "C" int orc_model_get_hidden(orc_model *m, int layer, float *out) {
   auto &v = m->hidden[layer];
   memcpy(out, v.data(), v.size() * sizeof(float));
   return (int)(v.size() / m->c.hidden);
+}
+
+extern "C" int orc_model_get_op(orc_model *m, int kind, int layer, float *out) {
+  if (kind < 2 || kind > 9 || layer < 0 || layer >= (int)m->ops[kind].size()) return -1;
+  const auto &v = m->ops[kind][layer];
+  if (out) memcpy(out, v.data(), v.size() * sizeof(float));
+  return m->ops_T;
 }
 
 extern "C" int orc_model_greedy(orc_model *m, int req, const int *prompt,

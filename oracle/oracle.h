@@ -65,6 +65,10 @@ void orc_linear(const float *X, const float *W, float *Y, int T, int N, int K,
 /* MMA block (products summed in fp32 per step) of the ORC_REF16 half
  * accumulator model; default 16 */
 void orc_set_ref_block(int k);
+/* fp32 summation order of orc_linear (tests only): 0 = dot8 (default),
+ * 1 = dot16 -- the same sums in another order, to measure how far ANY
+ * reordering moves the model (the noise floor of GPU-vs-oracle drift) */
+void orc_set_dot_variant(int v);
 /* Prompt-phase attention of one head (inc_multihead_self_attention.cu:98-366)
  * with the reference's half compute type: q [T_new][d] at positions
  * start..start+T_new-1, K/V [start+T_new][d], out [T_new][d]. */
@@ -126,6 +130,10 @@ int orc_model_decode_batch(orc_model *m, const int *reqs, const int *tokens,
 /* hidden state (residual stream before final norm) after layer `layer` of
  * the last forward call, [T][H]; layer == num_layers gives final-normed. */
 int orc_model_get_hidden(orc_model *m, int layer, float *out);
+/* per-op tensor of the last forward (kind = FFMI_DBG_* of include/ffmi.h,
+ * 2..9: attn_norm, qkv before RoPE [Q|K|V], attn_out, o_proj, ffn_norm,
+ * mlp_act, down, embed (layer 0)); returns T or -1; out NULL: T only */
+int orc_model_get_op(orc_model *m, int kind, int layer, float *out);
 /* greedy incremental decoding of one request: writes n_new tokens */
 int orc_model_greedy(orc_model *m, int req, const int *prompt, int n_prompt,
                      int n_new, int *out_tokens);

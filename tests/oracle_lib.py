@@ -67,11 +67,13 @@ def lib():
         L.orc_model_forward_ex.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p, ctypes.c_int,
                                            ctypes.c_int, _f32p, ctypes.c_int]
         L.orc_set_ref_block.argtypes = [ctypes.c_int]
+        L.orc_set_dot_variant.argtypes = [ctypes.c_int]
         L.orc_attention_prompt_ref16.argtypes = [_f32p, _f32p, _f32p] + [ctypes.c_int] * 3 + [
             _f32p]
         L.orc_model_decode_batch.argtypes = [ctypes.c_void_p, _i32p, _i32p, _i32p,
                                              ctypes.c_int, _f32p]
         L.orc_model_get_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.orc_model_get_op.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f32p]
         L.orc_model_greedy.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
                                        ctypes.c_int, ctypes.c_int, _i32p]
         L.orc_model_weight.restype = ctypes.c_long
@@ -94,6 +96,11 @@ REF16 = 2  # oracle.h ORC_REF16: the reference's half compute type in GEMMs / pr
 
 def set_ref_block(k):
     lib().orc_set_ref_block(k)
+
+
+def set_dot_variant(v):
+    """0: dot8 (default); 1: dot16 -- another fp32 summation order (noise floor)"""
+    lib().orc_set_dot_variant(v)
 
 
 def attention_prompt_ref16(q, K, V, start):
@@ -253,6 +260,20 @@ class Model:
     def hidden(self, layer, T):
         out = np.empty((T, self.cfg["hidden"]), np.float32)
         lib().orc_model_get_hidden(self.h, layer, fp(out))
+        return out
+
+    OPS = {"attn_norm": 2, "qkv": 3, "attn_out": 4, "o_proj": 5, "ffn_norm": 6, "mlp_act": 7,
+           "down": 8, "embed": 9}  # include/ffmi.h FFMI_DBG_*
+
+    def op(self, which, layer):
+        """per-op tensor of the last forward, [T][width] (see OPS)"""
+        k = self.OPS[which]
+        T = lib().orc_model_get_op(self.h, k, layer, None)
+        assert T > 0, (which, layer)
+        H, F = self.cfg["hidden"], self.cfg["intermediate"]
+        width = {3: 3 * H, 7: F}.get(k, H)
+        out = np.empty((T, width), np.float32)
+        lib().orc_model_get_op(self.h, k, layer, fp(out))
         return out
 
     def greedy(self, req, prompt, n_new):

@@ -193,7 +193,9 @@ def test_llama7b_width_batch8_tokens_match_oracle(oracle_7b, mode):
         exact += e
         total += n
     report("llama7b_width_batch8_tokens", mode=mode, exact=exact, total=total)
-    assert exact >= 0.95 * total, (exact, total)
+    # measured 280 / 280 in both modes (rounds 2 and 3); one noise-level tie
+    # allowed (each mismatch is checked as a <= 2-ulp tie above)
+    assert exact >= total - 1, (exact, total)
     llm.close()
 
 
@@ -202,9 +204,10 @@ def test_llama7b_width_tokens_vs_reference_half_semantics():
     cuBLAS half compute type in every dense layer, cuBLAS/cuDNN prompt
     attention, the generation kernel for decode steps), teacher-forced:
     each GPU token compared with what the reference would pick after the same
-    prefix.  The GPU accumulates in fp32 (DESIGN.md §7), so this is a measured
-    agreement, not bit-exactness; the bound below is the measured rate less a
-    margin, and the oracle's own fp32-accumulate mode shows the same gap."""
+    prefix.  The GPU accumulates in fp32 (DESIGN.md §8), so this is a measured
+    agreement, not bit-exactness; the bound below is the measured 63 / 66
+    less one token, and the oracle's own fp32-accumulate mode shows the same
+    gap."""
     ref = O.Model(LLAMA_7B_W, SEED_7B, fp16=O.REF16, max_requests=1, max_seq=160)
     ps = prompts(3, 32000, 20, 30, 17)
     llm = fa.Model(LLAMA_7B_W, "inc", max_requests=4, max_tokens=64, max_seq_len=128,
@@ -221,5 +224,5 @@ def test_llama7b_width_tokens_vs_reference_half_semantics():
         agree += int((ids[:len(gen)] == gen).sum())
         total += len(gen)
     report("llama7b_width_tokens_vs_ref16", agree=agree, total=total)
-    assert agree >= 0.85 * total, (agree, total)
+    assert total - agree <= 4, (agree, total)
     llm.close()

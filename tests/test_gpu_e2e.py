@@ -178,15 +178,28 @@ def test_spec_infer_equals_incr_on_gpu(ssm):
         spec, s_spec = run_spec(ps, 80, SSM_CFG, 5)
     else:  # SSM == LLM weights: near-100% acceptance exercises long accepted paths
         spec, s_spec = run_spec(ps, 80, LLM_CFG, 11)
+    # the reference's invariant (cpp_inference_tests.sh:183-189) is identity.
+    # The verify step runs its GEMMs on the M-split kernel (T = 84 here) and
+    # decoding on the skinny one (T = 4), which split K differently, so the
+    # fp32 sums -- and, at a near-tie, a greedy pick -- can differ (DESIGN.md
+    # §8, deviation 8).  Rule: identical, or the first divergence is a tie of
+    # the two tokens' fp16 probabilities within 2 ulp in the oracle, and the
+    # SpecInfer sequence is itself oracle-greedy up to such ties.
+    same = 0
     for p, a, b in zip(ps, inc, spec):
         n0 = len(p) + 1
-        if a.output_tokens != b.output_tokens:
-            # only a numerical tie may separate the two (different KV slot
-            # order -> different fp32 summation order); both must still be
-            # oracle-valid greedy sequences
-            check_tokens_vs_oracle(LLM_CFG, 11, b.output_tokens, n0)
-        else:
-            assert first_divergence(a.output_tokens, b.output_tokens) == len(a.output_tokens)
+        if a.output_tokens == b.output_tokens:
+            same += 1
+            continue
+        i = first_divergence(a.output_tokens, b.output_tokens)
+        assert i >= n0
+        m = O.Model(LLM_CFG, 11, fp16=1, max_requests=1, max_seq=len(a.output_tokens) + 1)
+        row = m.forward(0, np.array(a.output_tokens[:i], np.int32), 0)[-1]
+        pr = np.exp(row - row.max())
+        p16 = (pr / pr.sum()).astype(np.float16)
+        assert ulp_diff(p16[a.output_tokens[i]], p16[b.output_tokens[i]]) <= 2, i
+        check_tokens_vs_oracle(LLM_CFG, 11, b.output_tokens, n0)
+    report("spec_equals_incr", ssm=ssm, identical=same, requests=len(ps))
     if ssm == "same":
         assert s_inc.llm_steps >= 1.5 * s_spec.llm_steps  # cpp_inference_tests.sh:191-201
 

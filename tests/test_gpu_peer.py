@@ -51,9 +51,10 @@ CFG4 = dict(num_layers=2, vocab_size=1000, num_heads=4, num_kv_heads=4, hidden=2
                                      (8, 24, 32000, 3)])
 def test_vocab_shard_topk_matches_unsharded(n, T, V, k):
     """Vocab-parallel lm_head tail (model.cc:3392-3419): every rank's global
-    top-k ids and fp16 probabilities are bit-identical to the unsharded
-    softmax-argmax / top-k kernel, planted cross-shard ties included (lowest
-    index among equal fp16 probabilities)."""
+    top-k ids and fp16 probabilities are bit-identical to the oracle's softmax
+    + arg-top-k of the gathered logits (softmax.cu:262-288, arg_topk.cu:
+    339-448), planted cross-shard ties included (lowest index among equal fp16
+    probabilities)."""
     res = run_group(n, PT.vshard_task, (T, V, k, 1234 + n), max_bytes=1 << 20)
     ref_i, ref_p = res[0]["ref_ids"], res[0]["ref_probs"]
     for r in range(n):
@@ -117,3 +118,24 @@ def test_peer_tp8_llama65b_width_decodes_like_unsharded():
         assert len(toks) == 24
         check_tokens_vs_oracle(CFG65, 11, toks, len(p) + 1, tie_ulp=16,
                                max_tie_frac=0.1)
+
+
+def test_peer_tp8_llama65b_width_spec_infer_equals_incr():
+    """Config E's per-rank shapes: SpecInfer at LLaMA-65B widths over 8 rank
+    processes (tree-verify attention of 8 local heads, row-parallel halves
+    all-reduced over the transport, vocab-sharded tail, graphed verify steps)
+    with the LLaMA-68M-shaped SSM replicated on every rank, as the reference
+    runs its SSM at TP = 1 beside a TP LLM (spec_infer.cc:385-387).  Every
+    rank emits the same tokens, and they equal incremental decoding of the
+    same sharded model (cpp_inference_tests.sh:183-189).  (One SSM: the
+    reference's multi-SSM merge asserts, request_manager.cc:2823-2877.)"""
+    from test_gpu_e2e import prompts
+    ssm = dict(num_layers=2, vocab_size=32000, num_heads=12, num_kv_heads=12, hidden=768,
+               intermediate=3072, rms_eps=1e-6, rope_theta=10000.0)
+    ps = prompts(3, CFG65["vocab_size"], 4, 12, 5)
+    inc = run_group(8, PT.model_task, (CFG65, 11, ps, 28, False, ssm), max_bytes=8 << 20)
+    spec = run_group(8, PT.model_task, (CFG65, 11, ps, 28, True, ssm), max_bytes=8 << 20)
+    for r in range(8):
+        assert spec[r] == spec[0] and inc[r] == inc[0], r
+    assert spec[0] == inc[0]
+    assert all(len(t) == 28 for t in spec[0])

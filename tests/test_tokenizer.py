@@ -121,3 +121,27 @@ def test_benchmarking_tokens_prompt():
     assert r.input_tokens == [1] + [15] * 20 and len(r.output_tokens) == 40
     with pytest.raises(ValueError):
         rm.register_new_request(None, benchmarking_tokens=128)
+
+
+def test_bos_prefix_only_with_add_special_tokens(sp_dir, tmp_path):
+    """The "<s> " prefix needs add_special_tokens (request_manager.cc:776-781):
+    a caller-supplied BOS with add_special_tokens=False gets the bare text, in
+    the result and in the output-file record."""
+    tok = fa.load_tokenizer(str(sp_dir))
+    V = tok._sp.get_piece_size()
+    rm = fa.RequestManager(max_tokens_per_batch=16, max_requests_per_batch=4,
+                           max_sequence_length=128)
+    rm.register_tokenizer(str(sp_dir))
+    out = tmp_path / "out.txt"
+    rm.register_output_filepath(str(out))
+    ids = tok.encode("kalo mine suta")
+    g_plain = rm.register_new_request([1] + ids, max_length=20, add_special_tokens=False)
+    g_special = rm.register_new_request(ids, max_length=20)
+    rm.serve_incr_decoding(fa.HashModel(V, "inc", max_requests=4, max_seq_len=128))
+    plain, special = rm.get_generation_result(g_plain), rm.get_generation_result(g_special)
+    assert plain.output_tokens[0] == 1 and special.output_tokens[0] == 1
+    assert plain.output_text == tok._sp.decode(plain.output_tokens)
+    assert special.output_text == "<s> " + tok._sp.decode(special.output_tokens)
+    text = out.read_text()
+    assert special.output_text in text
+    assert "\n" + plain.output_text + "[Profile]" in text or text.endswith("\n" + plain.output_text)
