@@ -338,6 +338,7 @@ def main():
     fa.set_device(int(os.environ.get("FFMI_BENCH_DEVICE", local)))
     comm = None
     transport = "rccl"
+    transport_reason = "FFMI_TP_TRANSPORT=rccl"
     mode_tp = os.environ.get("FFMI_TP_TRANSPORT", "xgmi")  # xgmi | rccl | xgmi-only
     if world > 1:
         if mode_tp == "xgmi-only":
@@ -355,6 +356,7 @@ def main():
                 mine = comm.export(cap_tokens * hid * 2)
             except Exception as e:  # noqa: BLE001 -- reported, then agreed on below
                 print(f"[bench] rank {rank}: xGMI export failed ({e})", file=sys.stderr)
+                transport_reason = f"rank {rank}: xGMI export failed ({e})"
                 mine = b""
             handles = ctrl.allgather(mine)
             ok = 0.0
@@ -364,12 +366,20 @@ def main():
                     ok = 1.0
                 except Exception as e:  # noqa: BLE001
                     print(f"[bench] rank {rank}: xGMI attach failed ({e})", file=sys.stderr)
+                    transport_reason = f"rank {rank}: xGMI attach failed ({e})"
+            elif mine:
+                transport_reason = "another rank's xGMI export failed"
             if -ctrl.max(-ok) < 1.0:  # some rank failed: every rank stays on RCCL
                 if mode_tp == "xgmi-only":
                     raise SystemExit("xGMI transport failed and FFMI_TP_TRANSPORT=xgmi-only")
                 comm.detach()
+                if transport_reason.startswith("FFMI"):
+                    transport_reason = "another rank's xGMI attach failed"
+                # every rank reports rank 0's view; the reason of the failing
+                # rank is on that rank's stderr
             else:
                 transport = "xgmi"
+                transport_reason = "direct xGMI all-reduce attached on every rank"
 
     llm_cfg = fa.llama_config_from_hf(args.llm_weights) if args.llm_weights else dict(LLAMA_7B)
     ssm_cfg = fa.llama_config_from_hf(args.ssm_weights) if args.ssm_weights else dict(LLAMA_68M)
@@ -458,7 +468,9 @@ def main():
                             else "LLaMA-68M (random init)") if spec else None),
                    "global_batch": B, "prefill": P, "decode": D, "seq_len": max_len,
                    "parallelism": f"tp{world}",
-                   "tp_transport": transport if world > 1 else None, "tree_widths": list(widths) if spec else None,
+                   "tp_transport": transport if world > 1 else None,
+                   "tp_transport_reason": transport_reason if world > 1 else None,
+                   "tree_widths": list(widths) if spec else None,
                    "max_tokens_per_batch": mtb, "layers": llm_cfg["num_layers"]},
         "p50_token_latency_ms": round(statistics.median(lats) / 1000.0, 3),
         "llm_steps_per_generate": llm_steps / args.steps,

@@ -846,6 +846,7 @@ bool comm_has_peer(const ffmi_comm *c, size_t bytes) {
 int comm_size(const ffmi_comm *c) { return c ? c->nranks : 1; }
 bool comm_peer_attached(const ffmi_comm *c) { return c && c->peer && c->peer->attached; }
 bool comm_has_fallback(const ffmi_comm *c) { return c && (c->comm || c->local); }
+bool comm_is_rccl(const ffmi_comm *c) { return c && c->comm && !c->local; }
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
                                 int ld, int col0, int dtype, hipStream_t s) {
   return peer_run(c, in, out, rows, cols, ld, col0, dtype, s);
@@ -902,7 +903,7 @@ extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, s
   FFMI_CHECK(c->local || c->comm || c->nranks == 1, FFMI_ERR_INVALID);
   if (c->local && c->nranks > 1)
     return local_allreduce(c, in, out, count, dtype, (hipStream_t)stream);
-  if (c->nranks == 1) {
+  if (c->nranks == 1 && !c->comm) {
     if (in != out) {
       const size_t esz = dtype == FFMI_F16 ? 2 : 4;
       FFMI_HIP(hipMemcpyAsync(out, in, count * esz, hipMemcpyDeviceToDevice, (hipStream_t)stream));

@@ -222,6 +222,8 @@ int comm_size(const ffmi_comm *c);
 bool comm_peer_attached(const ffmi_comm *c);
 // an RCCL communicator or an in-process group takes what the transport cannot
 bool comm_has_fallback(const ffmi_comm *c);
+// an RCCL communicator (stream-capturable all-reduce)
+bool comm_is_rccl(const ffmi_comm *c);
 // sum of every rank's [rows][cols] `in` into `out` (row stride ld, starting
 // at column col0) over the xGMI transport
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,

@@ -8,8 +8,10 @@
 // softmax+arg_top_k (SSM, llama.cc:277-295).
 // Tensor parallelism (model.cc:3392-3613, linear.cc:1691-1730): qkv/gate/up
 // column-parallel (heads / FFN columns of shard `tp_rank`), o/down
-// row-parallel followed by an RCCL sum all-reduce; norms replicated; lm_head
-// replicated (the reference vocab-shards it and Combines).
+// row-parallel followed by a sum all-reduce -- the direct xGMI transport
+// (collective.hip) or RCCL, both in two column halves overlapped on a second
+// stream and captured in the step's HIP graph; norms replicated; lm_head
+// vocab-sharded with the sharded softmax / top-k tail (model.cc:3392-3419).
 #include <stdio.h>
 #include <string.h>
 
@@ -62,6 +64,11 @@ struct LlamaGPU : public ffmi_model {
   // comm_stream while the next half computes (allreduce.cc:291-331 runs the
   // collective as a concurrent task; here it overlaps on HIP streams)
   bool peer = false;
+  // RCCL all-reduce (no transport attached, or the transport cannot hold a
+  // step): the same two-half overlap and graph capture as over the transport
+  // (ncclAllReduce is stream-capturable); an in-process local group is not
+  // (its all-reduce synchronises the host) and runs eager and unsplit
+  bool rccl = false;
   int tp_chunks = 1;
   hipStream_t comm_stream = nullptr;
   uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
@@ -387,7 +394,8 @@ struct LlamaGPU : public ffmi_model {
                           "RCCL communicator", __FILE__, __LINE__);
       return FFMI_ERR_INVALID;
     }
-    if (peer) {
+    rccl = P > 1 && !peer && ffmi::comm_is_rccl(o.comm);
+    if (peer || rccl) {
       tp_chunks = 2;
       if (const char *e = getenv("FFMI_TP_OVERLAP")) tp_chunks = atoi(e) ? 2 : 1;
       if ((H / tp_chunks) % 32 != 0) tp_chunks = 1;
@@ -515,7 +523,7 @@ struct LlamaGPU : public ffmi_model {
   ffmi_status rowpar_gemm_allreduce(const uint16_t *X, const uint16_t *W, int K, uint16_t *out,
                                     int T, int XP) {
     const int H = c.hidden;
-    if (!peer || tp_chunks == 1) {
+    if (!(peer || rccl) || tp_chunks == 1) {
       FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream, nullptr));
       if (peer) return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream);
       return allreduce(out, (size_t)T * H);
@@ -529,9 +537,17 @@ struct LlamaGPU : public ffmi_model {
                                  nullptr, H / 16));
       FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
       FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
-      ffmi_status st =
-          ffmi::comm_allreduce_cols(o.comm, cb, out, T, Hc, H, ch * Hc, FFMI_F16, comm_stream);
-      if (st != FFMI_OK) return st;
+      if (peer) {  // the transport reduces straight into out's columns
+        ffmi_status st =
+            ffmi::comm_allreduce_cols(o.comm, cb, out, T, Hc, H, ch * Hc, FFMI_F16, comm_stream);
+        if (st != FFMI_OK) return st;
+      } else {  // RCCL: contiguous in place, then into out's columns
+        ffmi_status st = ffmi_allreduce(o.comm, cb, cb, (size_t)T * Hc, FFMI_F16,
+                                        (ffmi_stream)comm_stream);
+        if (st != FFMI_OK) return st;
+        FFMI_HIP(hipMemcpy2DAsync(out + (size_t)ch * Hc, (size_t)H * 2, cb, (size_t)Hc * 2,
+                                  (size_t)Hc * 2, T, hipMemcpyDeviceToDevice, comm_stream));
+      }
     }
     FFMI_HIP(hipEventRecord(ev_comm_done, comm_stream));
     FFMI_HIP(hipStreamWaitEvent(stream, ev_comm_done, 0));
@@ -578,7 +594,7 @@ struct LlamaGPU : public ffmi_model {
     // request (a fixed shape while the batch is full: T = 168 for 8 requests
     // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
     const bool graph = use_graphs && !dbg && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
-                       (o.tp_size == 1 || peer) && !prof_on(0, T) &&
+                       (o.tp_size == 1 || peer || rccl) && !prof_on(0, T) &&
                        !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
@@ -712,6 +728,19 @@ struct LlamaGPU : public ffmi_model {
     TRY(ffmi_linear_ws(h, lm, logits, T, Vl, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, Vl, Vl, H), 2.0 * T * Vl * H);
     pr = prof_begin(ptail);
+    TRY(enqueue_sampling(k, T));
+    prof_end(pr, SAMPLING, (double)T * V * 2, 0);
+#undef TRY
+    return FFMI_OK;
+  }
+
+  // softmax + argmax / arg-top-k of the step's logits into the pinned results
+  ffmi_status enqueue_sampling(int k, int T) {
+    const int V = c.vocab_size;
+    const ffmi_stream s = (ffmi_stream)stream;
+    ffmi_status st;
+#define TRY(x) \
+  do { if ((st = (x)) != FFMI_OK) return st; } while (0)
     // ids [T*k] then probs [T*k] back to back.  The sampling kernel writes
     // them straight into the pinned host buffer (a few bytes per row over
     // PCIe, visible after the stream synchronisation like a copy kernel's
@@ -727,7 +756,6 @@ struct LlamaGPU : public ffmi_model {
     } else {
       TRY(ffmi_arg_topk(logits, T, V, k, ids_o, probs_o, s));
     }
-    prof_end(pr, SAMPLING, (double)T * V * 2, 0);
     if (result_copy)
       FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));
 #undef TRY

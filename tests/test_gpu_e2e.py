@@ -295,3 +295,4 @@ def test_result_copy_modes_same_tokens(monkeypatch, graphs):
         out.append(([r.output_tokens for r in inc], [r.output_tokens for r in spec]))
     assert out[0] == out[1]
     assert out[0][0] == out[0][1]  # and SpecInfer == incremental decoding
+

@@ -88,3 +88,41 @@ def test_tp2_spec_infer_tokens_are_greedy():
     for p, x in zip(ps, res[0]):
         check_tokens_vs_oracle(LLM_CFG, 11, x.output_tokens, len(p) + 1, tie_ulp=4,
                                max_tie_frac=0.1)
+
+
+@pytest.mark.parametrize("spec", [False, True])
+def test_rccl_shard_graphed_overlapped_equals_eager(monkeypatch, spec):
+    """The RCCL all-reduce path (no xGMI transport attached): row-parallel
+    GEMMs in two column halves, each ncclAllReduce'd on the second stream
+    and copied into its columns, the whole step captured in a HIP graph --
+    the same schedule as over the transport.  RCCL refuses two ranks on one
+    GPU, so this is shard 0 of TP = 2 over a one-rank RCCL communicator
+    (ncclAllReduce of one rank still runs): graphed + overlapped, unsplit,
+    and eager runs must give identical tokens."""
+    cfg = dict(CFG4, vocab_size=1024)  # vocab-sharded lm_head: the tail all-reduces too
+    ps = prompts(3, cfg["vocab_size"], 5, 30, 13)
+    extra = 23 * 4 if spec else 0
+
+    def run():
+        uid = fa.Comm.unique_id()
+        comm = fa.Comm(uid, 1, 0)
+        m = fa.Model(cfg, "tree" if spec else "inc", max_requests=4, max_tokens=32 + extra,
+                     max_seq_len=128, weight_seed=11, tp_rank=0, tp_size=2, comm=comm)
+        rm = fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=32,
+                               max_sequence_length=128, spec_tree_width=(1, 1, 3) if spec else ())
+        if spec:
+            rm.register_ssm_model(fa.Model(dict(SSM_CFG, vocab_size=cfg["vocab_size"]), "beam",
+                                           max_requests=4, max_tokens=32 + extra,
+                                           max_seq_len=128, weight_seed=5))
+        out = [r.output_tokens for r in fa.generate(rm, m, ps, max_length=56)]
+        m.close()
+        comm.close()
+        return out
+
+    base = run()
+    monkeypatch.setenv("FFMI_TP_OVERLAP", "0")
+    unsplit = run()
+    monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
+    eager = run()
+    assert base == unsplit == eager
+    assert all(len(t) == 56 for t in base)
