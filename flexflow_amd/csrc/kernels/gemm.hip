@@ -322,6 +322,93 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
   return hipGetLastError();
 }
 
+// Wide, short-K layers (the 68M SSM's lm_head: 2000 tiles, K = 768): one
+// WAVE per group of NT tiles over the whole K (a single MFMA chain per tile,
+// no cross-wave reduction, no LDS), four independent waves per workgroup.
+// The K-split form launches 1000 short 4-wave workgroups whose loads never
+// fill the CU (13 us for 49 MB from the Infinity Cache); here each wave keeps
+// two batches of UB k-steps in flight (double-buffered registers).
+template <int MT, int NT, int UB, bool NTL>
+__global__ __launch_bounds__(256) void gemm_wave_kernel(const uint16_t *__restrict__ X,
+                                                        const uint16_t *__restrict__ Wp,
+                                                        uint16_t *__restrict__ Y, int T, int N,
+                                                        int KT, int NTILES, int xp, int yp,
+                                                        size_t wts, size_t wks) {
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g * NT >= NTILES) return;
+  const int XS = xp ? 512 : 32;
+  const uint16_t *xrow[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) {
+    if (xp) {
+      xrow[i] = X + ((size_t)min(i, (T - 1) >> 4) * KT * 64 + lane) * 8;
+    } else {
+      const int r = min(i * 16 + (lane & 15), T - 1);
+      xrow[i] = X + (size_t)r * (KT * 32) + 8 * (lane >> 4);
+    }
+  }
+  const uint16_t *wrow[NT];
+#pragma unroll
+  for (int j = 0; j < NT; ++j) wrow[j] = Wp + (size_t)min(g * NT + j, NTILES - 1) * wts + lane * 8;
+  f4 acc[MT][NT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i)
+#pragma unroll
+    for (int j = 0; j < NT; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+  h8 bA[UB][NT], xA[UB][MT], bB[UB][NT], xB[UB][MT];
+  auto ld = [&](h8(&bb)[UB][NT], h8(&xx)[UB][MT], int k0) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      const int kk = min(k0 + u, KT - 1);
+#pragma unroll
+      for (int j = 0; j < NT; ++j) bb[u][j] = ld_weight<NTL>(wrow[j] + (size_t)kk * wks);
+#pragma unroll
+      for (int i = 0; i < MT; ++i) xx[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
+    }
+  };
+  const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+  auto mm = [&](h8(&bb)[UB][NT], h8(&xx)[UB][MT], int k0) {
+#pragma unroll
+    for (int u = 0; u < UB; ++u) {
+      if (k0 + u >= KT) {  // past K: re-loaded fragments times a zero weight
+#pragma unroll
+        for (int j = 0; j < NT; ++j) bb[u][j] = zero;
+      }
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int j = 0; j < NT; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xx[u][i], bb[u][j], acc[i][j], 0, 0, 0);
+    }
+  };
+  ld(bA, xA, 0);
+  for (int k0 = 0; k0 < KT; k0 += 2 * UB) {
+    if (k0 + UB < KT) ld(bB, xB, k0 + UB);
+    __builtin_amdgcn_sched_barrier(0);
+    mm(bA, xA, k0);
+    __builtin_amdgcn_sched_barrier(0);
+    if (k0 + 2 * UB < KT) ld(bA, xA, k0 + 2 * UB);
+    __builtin_amdgcn_sched_barrier(0);
+    if (k0 + UB < KT) mm(bB, xB, k0 + UB);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // C layout: column lane & 15, rows (lane >> 4) * 4 + r
+#pragma unroll
+  for (int j = 0; j < NT; ++j) {
+    const int n = (g * NT + j) * 16 + (lane & 15);
+    if (g * NT + j >= NTILES || n >= N) continue;
+#pragma unroll
+    for (int i = 0; i < MT; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = i * 16 + (lane >> 4) * 4 + r;
+        if (m < T)
+          Y[yp ? act_packed_off(m, n, N) : (size_t)m * N + n] = __half_as_ushort(__float2half_rn(acc[i][j][r]));
+      }
+  }
+}
+
 // Split-K factor of the skinny path: only narrow layers (few column groups,
 // e.g. the 68M SSM's o/down with 48 tiles) and only when the consumer takes
 // the partial slabs (no reduce pass); keeps >= 4 k-steps per wave.
@@ -360,6 +447,23 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
     if (fnt == 4 && fkw == 4) return run<MT, 4, 4, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
     if (fnt == 4 && fkw == 2) return run<MT, 4, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
     if (fnt == 2 && fkw == 2) return run<MT, 2, 2, U, 0>(X, Wp, Y, ws, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch);
+  }
+  // wide, short-K layers (the SSM lm_head): one wave per 2 tiles over the
+  // whole K (gemm_wave_kernel; FFMI_WAVE_GEMM=0 keeps the K-split form)
+  static const bool wave_ok = !getenv("FFMI_WAVE_GEMM") || atoi(getenv("FFMI_WAVE_GEMM")) != 0;
+  if (wave_ok && ntiles >= 1024 && KT <= 32 && S == 1) {
+    const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch);
+    // two tiles per wave: SSM lm_head (32000 x 768) at T = 24 11.1 us (13.3
+    // in the K-split form, 13.3 with one tile per wave and twice the waves),
+    // T = 8 9.4 us (12.5)
+    const int groups = (ntiles + 1) / 2;
+#define FFMI_WAVE(NL)                                                                      \
+  hipLaunchKernelGGL((gemm_wave_kernel<MT, 2, 4, NL>), dim3((groups + 3) / 4), dim3(256), 0, s, \
+                     X, Wp, Y, T, N, KT, ntiles, xp, yp, wts, wks)
+    if (nt) FFMI_WAVE(true);
+    else FFMI_WAVE(false);
+#undef FFMI_WAVE
+    return hipGetLastError();
   }
   // wide layers (lm_head): two tiles per workgroup once there are >= 2 row
   // tiles (SSM lm_head at T = 24: 16.1 -> 12.3 us warm; at one row tile a

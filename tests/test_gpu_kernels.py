@@ -74,6 +74,28 @@ def test_linear_matches_oracle(T, N, K):
     close16(Yb.get(), ref)
 
 
+@pytest.mark.parametrize("T", [1, 8, 24, 33, 64])
+@pytest.mark.parametrize("N,K", [(32000, 768), (32001, 1024), (16384, 64)])
+@pytest.mark.parametrize("xp", [0, 1])
+def test_linear_wide_short_k_wave_form(T, N, K, xp):
+    """Wide, short-K layers (>= 1024 tiles, K <= 1024: the 68M SSM's
+    lm_head) run one wave per tile pair over the whole K
+    (gemm_wave_kernel): within 2 fp16 ulp of the oracle, row-major or packed
+    activations, ragged N and T, odd tile counts."""
+    rng = np.random.default_rng(T + N + K + xp)
+    X = f16(rng.standard_normal((T, K)))
+    W = f16(rng.uniform(-0.05, 0.05, (N, K)))
+    Wp = packed(W)
+    Xb, Yb = Buf(X), Buf.empty((T, N), np.float16)
+    flags = F.EPI_NONE
+    if xp:
+        Xb = Buf(pack_act_np(X))
+        flags |= F.X_PACKED
+    F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Yb.ptr, T, N, K, flags, None))
+    ref = O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1)
+    close16(Yb.get(), ref)
+
+
 @pytest.mark.parametrize("T", [65, 100, 168, 200])
 @pytest.mark.parametrize("epi", [0, 1])
 def test_linear_packed_activations_bit_identical(T, epi):
