@@ -59,7 +59,10 @@ extern "C" ffmi_status ffmi_batch_create(int max_tokens, int max_requests, ffmi_
            align16((size_t)max_tokens * sizeof(ffmi::WorkDev)) +
            align16((size_t)max_tokens * sizeof(ffmi_commit_info)) +
            align16((size_t)max_requests * FFMI_MAX_TREE * sizeof(uint64_t)) + 64;
-  if (hipHostMalloc((void **)&b->host, b->cap, hipHostMallocDefault) != hipSuccess ||
+  // fine-grained (uncached on the device) and mapped: the model's first
+  // kernel reads the step's blob straight from here (launch_rmsnorm's fetch)
+  if (hipHostMalloc((void **)&b->host, b->cap, hipHostMallocCoherent | hipHostMallocMapped) !=
+          hipSuccess ||
       hipMalloc((void **)&b->dev, b->cap) != hipSuccess) {
     delete b;
     ffmi_set_last_error("batch alloc", __FILE__, __LINE__);

@@ -159,7 +159,8 @@ size_t packed_act_bytes(int T, int K);
 hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s);
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s, bool out_packed = false, Partials x2p = {}, const char *gather = nullptr);
+                          hipStream_t s, bool out_packed = false, Partials x2p = {}, const char *gather = nullptr,
+                          char *blob_dst = nullptr, size_t blob_bytes = 0);
 hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
                             uint16_t *out, int H, hipStream_t s);
 hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,

@@ -43,7 +43,8 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
     uint16_t *__restrict__ out, int H, float eps, int out_packed,
-    const float *__restrict__ x2p, int pS, int pNP, const char *__restrict__ gather) {
+    const float *__restrict__ x2p, int pS, int pNP, const char *__restrict__ gather,
+    uint4 *__restrict__ blob_dst, int blob_n16) {
   __shared__ float scratch[NT / 64];
   const int row = blockIdx.x;
   const int T = gridDim.x;
@@ -52,6 +53,14 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   // embedding lookup fused into the first layer's norm; res_out gets the copy)
   const uint16_t *a = SRC == 3 ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
                                : x1 + (size_t)row * H;
+  // blob fetch: gather is the step's staging blob in mapped host memory; the
+  // grid copies it into device memory for the step's later kernels (replaces
+  // the H2D copy node and the system-scope boundary after it), its loads in
+  // flight together with the token-id read
+  if (SRC == 3 && blob_dst) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(gather);
+    for (int i = row * NT + threadIdx.x; i < blob_n16; i += T * NT) blob_dst[i] = src[i];
+  }
   uint4 v[MAXC], wv[MAXC];
   // every load of the row first (slabs, x2, x1, w), then the arithmetic;
   // x2 = the deferred split-K slabs of the producing GEMM summed in order,
@@ -139,8 +148,15 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
-                          hipStream_t s, bool out_packed, Partials x2p, const char *gather) {
+                          hipStream_t s, bool out_packed, Partials x2p, const char *gather,
+                          char *blob_dst, size_t blob_bytes) {
   if (gather && (x2 || x2p.S > 0 || !res_out)) return hipErrorInvalidValue;
+  if (blob_dst && (!gather || blob_bytes > (size_t)1 << 30 || (uintptr_t)gather % 16 ||
+                   (uintptr_t)blob_dst % 16))
+    return hipErrorInvalidValue;
+  // whole 16-byte chunks: the staging and device blobs are 16-aligned and
+  // padded (ffmi_batch_create), so the rounded-up tail stays inside both
+  const int blob_n16 = blob_dst ? (int)((blob_bytes + 15) / 16) : 0;
   if (T <= 0) return hipSuccess;
   if (out_packed && H % 32) return hipErrorInvalidValue;
   const int op = out_packed ? 1 : 0;
@@ -156,7 +172,8 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   const int ms = !pp || x2p.S <= 1 ? 1 : x2p.S <= 2 ? 2 : x2p.S <= 4 ? 4 : 8;
 #define FFMI_RMS3(NT, MC, MS, SR)                                                              \
   hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS, SR>), dim3(T), dim3(NT), 0, s, x1, x2, w,    \
-                     res_out, out, H, eps, op, pp, x2p.S, x2p.NP, gather)
+                     res_out, out, H, eps, op, pp, x2p.S, x2p.NP, gather,               \
+                     reinterpret_cast<uint4 *>(blob_dst), blob_n16)
 #define FFMI_RMS(NT, MC)                                   \
   do {                                                     \
     if (src == 0) FFMI_RMS3(NT, MC, 1, 0);                 \

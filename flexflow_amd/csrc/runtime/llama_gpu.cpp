@@ -572,6 +572,7 @@ struct LlamaGPU : public ffmi_model {
   int tree_parity = 0;
   std::map<GraphKey, hipGraphExec_t> graphs;
   bool use_graphs = getenv("FFMI_NO_GRAPHS") == nullptr;
+  bool blob_fetch = !getenv("FFMI_BLOB_FETCH") || atoi(getenv("FFMI_BLOB_FETCH")) != 0;
   // largest one-item-per-request step that is graphed (FFMI_GRAPH_MAXT: A/B)
   int graph_max_t = getenv("FFMI_GRAPH_MAXT") ? atoi(getenv("FFMI_GRAPH_MAXT")) : 1024;
 
@@ -594,7 +595,8 @@ struct LlamaGPU : public ffmi_model {
     // request (a fixed shape while the batch is full: T = 168 for 8 requests
     // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
     const bool graph = use_graphs && !dbg && (T <= 64 || (batch->one_item_per_req && T <= graph_max_t)) &&
-                       (o.tp_size == 1 || peer || rccl) && !prof_on(0, T) &&
+                       (o.tp_size == 1 || peer || rccl || ffmi::comm_size(o.comm) == 1) &&
+                       !prof_on(0, T) &&
                        !prof_on(c.num_layers / 2, T);
     if (graph) {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
@@ -645,7 +647,9 @@ struct LlamaGPU : public ffmi_model {
     ffmi_status st;
 #define TRY(x) \
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
-    TRY(ffmi::batch_copy(batch, blob_bytes, stream, record_upload));
+    // the step's blob: fetched by the first kernel from the mapped staging
+    // (default), or a separate H2D copy (FFMI_BLOB_FETCH=0: A/B)
+    if (!blob_fetch) TRY(ffmi::batch_copy(batch, blob_bytes, stream, record_upload));
     const bool ptail = prof_on(0, T);
     int pr = 0;
     ffmi::Partials down_part;
@@ -662,7 +666,10 @@ struct LlamaGPU : public ffmi_model {
       FFMI_HIP(ffmi::launch_rmsnorm(l == 0 ? embed : res, l == 0 ? nullptr : proj, L.in_norm, res,
                                     h, T, H, eps, stream, packed,
                                     l == 0 ? ffmi::Partials() : down_part,
-                                    l == 0 ? batch->dev : nullptr));
+                                    l == 0 ? (blob_fetch ? batch->host : batch->dev) : nullptr,
+                                    l == 0 && blob_fetch ? batch->dev : nullptr, blob_bytes));
+      // the staging is free for the next step once the fetch has read it
+      if (l == 0 && blob_fetch && record_upload) FFMI_HIP(hipEventRecord(batch->uploaded, stream));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
       if (dbg) {
         // residual stream after layer l-1 (layer 0: the embedding rows)

@@ -1,9 +1,12 @@
 """Per-rank compute of the TP=N SpecInfer step, on ONE GPU.
 
 Builds the LLaMA-7B (or --model 65b: LLaMA-65B, configs D/E) verify model as shard 0 of N (heads / FFN columns /
-rows of o and down) over a 1-rank communicator, so its all-reduces are
-no-ops: the numbers are the per-rank GEMM / attention / norm time of the
-bench at --gpus N, WITHOUT the all-reduce cost (tokens are meaningless).
+rows of o and down) over a 1-rank communicator with no RCCL state and no
+transport (Comm.peer(1, 0), never attached), so its all-reduces are no-ops and
+its steps are graphed like the bench's: the numbers are the per-rank GEMM /
+attention / norm time of the bench at --gpus N, WITHOUT the all-reduce cost
+(tokens are meaningless).  (Round 3's first table used a 1-rank RCCL
+communicator, which now takes the RCCL path and times ncclAllReduce calls.)
 
     python scripts/tp_shard_bench.py --tp 8 [--model 65b] [--mode incr]
 """
@@ -30,7 +33,7 @@ def main():
     cfg = LLAMA_65B if args.model == "65b" else LLAMA_7B
     spec = args.mode == "spec"
     fa.set_device(0)
-    comm = stdout_to_stderr(lambda: fa.Comm(stdout_to_stderr(fa.Comm.unique_id), 1, 0))
+    comm = fa.Comm.peer(1, 0)
     B, P, D, tree, mtb = 8, 128, 128, 23, 1024
     rm_kw = dict(max_requests_per_batch=B, max_tokens_per_batch=mtb,
                  max_spec_tree_token_num=tree, max_sequence_length=512)
