@@ -24,7 +24,10 @@ run bench 400 python bench.py && grep '^{' gpurun_out/bench.log | tail -1 > "gpu
  timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/prof" -o bench -- python3 $B --warmup 1 > "$R/gpurun_out/prof.log" 2>&1 && \
  cp "$P/prof/bench_kernel_stats.csv" "$R/gpurun_out/${TAG}_bench_kernel_stats.csv" && echo "[prof] ok" && \
  timeout -k 10 400 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$P/pmc" -o bench -- python3 $B --warmup 0 > "$R/gpurun_out/pmc.log" 2>&1 && \
- python3 "$R/scripts/pmc_summary.py" "$P/pmc/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_fetch.json" && echo "[pmc] ok" && \
+ python3 "$R/scripts/pmc_summary.py" "$P/pmc/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_fetch.json" && \
+ python3 "$R/scripts/pmc_table.py" "$P/pmc/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_fetch_table.json" && echo "[pmc] ok" && \
+ timeout -k 10 400 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$P/pmcw" -o bench -- python3 $B --warmup 0 > "$R/gpurun_out/pmc_w.log" 2>&1 && \
+ python3 "$R/scripts/pmc_table.py" "$P/pmcw/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_write_table.json" && echo "[pmc write] ok" && \
  timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$P/mfma" -o bench -- python3 $B --warmup 0 > "$R/gpurun_out/pmc_mfma.log" 2>&1 && \
  python3 "$R/scripts/mfma_summary.py" "$P/mfma/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_mfma.json" && echo "[pmc_mfma] ok" && \
  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/incr" -o incr -- python3 "$R/bench.py" --mode incr --steps 1 --warmup 1 --no-cpu-baseline --profile 0 > "$R/gpurun_out/incr_prof.log" 2>&1 && \

@@ -87,8 +87,13 @@ def _usage(src):
                     reason="hipcc not available")
 def test_no_kernel_uses_scratch():
     srcs = sorted(os.path.join(KDIR, f) for f in os.listdir(KDIR) if f.endswith(".hip"))
+    # the library is fresh only if newer than every kernel source AND every
+    # header the kernels include (a WorkDev / collective layout change)
+    csrc = os.path.dirname(KDIR)
+    hdrs = [os.path.join(d, f) for d in (csrc, KDIR, os.path.join(ROOT, "include"))
+            for f in os.listdir(d) if f.endswith(".h")]
     fresh = os.path.exists(LIB) and os.path.exists(f"{LLVM}/llvm-readelf") and \
-        all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs)
+        all(os.path.getmtime(LIB) >= os.path.getmtime(s) for s in srcs + hdrs)
     if fresh:
         results = [_lib_usage(LIB)]
     else:
