@@ -930,6 +930,8 @@ extern "C" long ffmi_debug_attn_stamps(long long *dst, long max_waves) {
   return ffmi::attn_debug_stamps(dst, max_waves);
 }
 
+extern "C" long ffmi_debug_markers(long long *dst, long n) { return ffmi::debug_markers(dst, n); }
+
 extern "C" size_t ffmi_packed_activation_bytes(int T, int in_dim) {
   return T > 0 && in_dim > 0 ? ffmi::packed_act_bytes(T, in_dim) : 0;
 }

@@ -154,6 +154,9 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
 // rounded once: the value every consumer of the slabs computes (tensor capture)
 hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, hipStream_t s);
 long attn_debug_stamps(long long *dst, long max_waves);
+hipError_t launch_marker(int i, hipStream_t s);
+void attn_stamp_gate(bool open);
+long debug_markers(long long *dst, long n);
 long gemm_debug_stamps(long long *dst, long max_waves);
 size_t packed_act_bytes(int T, int K);
 hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStream_t s);

@@ -786,7 +786,10 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 0>), grid, dim3(512), 0, s,    \
                          blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
   } while (0)
-  if (kv.stamps && D == 128) {  // diagnostics build of the verify / decode kernels
+  // diagnostics build: FFMI_ATTN_STAMP=1 stamps the d = 128 (LLM) launches,
+  // FFMI_ATTN_STAMP=64 the d = 64 (68M SSM) ones
+  static const int stamp_d = getenv("FFMI_ATTN_STAMP") && atoi(getenv("FFMI_ATTN_STAMP")) == 64 ? 64 : 128;
+  if (kv.stamps && D == stamp_d) {
 #define FFMI_ATT_ST(QT)                                                                         \
   do {                                                                                          \
     if (fused)                                                                                  \
@@ -818,12 +821,39 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
 // V^T stores, HW_ID, chunks} (100 MHz realtime) for ffmi_debug_attn_stamps.
 static long long *g_attn_stamps = nullptr;
 static long g_attn_stamp_waves = 0;
+static bool g_attn_stamp_gate = true;
+// the model closes the gate for every launch but the one its markers bracket
+void attn_stamp_gate(bool open) { g_attn_stamp_gate = open; }
 static long long *attn_stamp_buf(int wgs) {
   static const bool on = getenv("FFMI_ATTN_STAMP") != nullptr;
-  if (!on) return nullptr;
+  if (!on || !g_attn_stamp_gate) return nullptr;
   if (!g_attn_stamps && hipMalloc(&g_attn_stamps, (size_t)8 << 20) != hipSuccess) return nullptr;
   g_attn_stamp_waves = std::min<long>((long)wgs * 8, ((long)8 << 20) / 96);
   return g_attn_stamps;
+}
+
+// FFMI_MARKERS=1 diagnostics: a one-wave kernel that records the 100 MHz
+// realtime clock (the attention stamps' clock) into slot i when it starts,
+// enqueued between the kernels of the model's last layer: with the wave
+// stamps it splits a launch's duration into boundary and in-kernel time.
+__global__ void marker_kernel(long long *buf, int i) {
+  if (threadIdx.x == 0) buf[i] = __builtin_amdgcn_s_memrealtime();
+}
+static long long *g_markers = nullptr;
+hipError_t launch_marker(int i, hipStream_t s) {
+  if (i < 0 || i >= 64) return hipErrorInvalidValue;
+  if (!g_markers && hipMalloc(&g_markers, 64 * sizeof(long long)) != hipSuccess)
+    return hipErrorOutOfMemory;
+  hipLaunchKernelGGL(marker_kernel, dim3(1), dim3(64), 0, s, g_markers, i);
+  return hipGetLastError();
+}
+long debug_markers(long long *dst, long n) {
+  if (!g_markers || n <= 0) return 0;
+  n = std::min<long>(n, 64);
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(dst, g_markers, (size_t)n * sizeof(long long), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
+  return n;
 }
 
 long attn_debug_stamps(long long *dst, long max_waves) {

@@ -653,9 +653,22 @@ struct LlamaGPU : public ffmi_model {
     const bool ptail = prof_on(0, T);
     int pr = 0;
     ffmi::Partials down_part;
+    // FFMI_MARKERS=<hidden>: clock markers between the last layer's kernels
+    // of the model with that hidden size (diagnostics, ffmi_debug_markers)
+    // (FFMI_MARKERS_T: only steps of that many tokens, e.g. 168 = a full
+    // verify batch; the attention stamps then come from the same launch)
+    static const int marker_h = getenv("FFMI_MARKERS") ? atoi(getenv("FFMI_MARKERS")) : 0;
+    static const int marker_t = getenv("FFMI_MARKERS_T") ? atoi(getenv("FFMI_MARKERS_T")) : 0;
+    int mark_i = 0;
     for (int l = 0; l < c.num_layers; ++l) {
       Layer &L = layers[l];
       const bool on = prof_on(l, T);
+      const bool mark_on = marker_h == c.hidden && l == c.num_layers - 1 && (!marker_t || T == marker_t);
+      if (marker_h) ffmi::attn_stamp_gate(mark_on);
+      auto mk = [&]() {
+        if (mark_on) (void)ffmi::launch_marker(mark_i++, stream);
+      };
+      mk();
       pr = prof_begin(on);
       // split-K GEMMs leave their partial slabs for the next kernel to combine
       // (rope-store for qkv; the residual norm for o/down when there is no
@@ -671,6 +684,7 @@ struct LlamaGPU : public ffmi_model {
       // the staging is free for the next step once the fetch has read it
       if (l == 0 && blob_fetch && record_upload) FFMI_HIP(hipEventRecord(batch->uploaded, stream));
       prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
+      mk();
       if (dbg) {
         // residual stream after layer l-1 (layer 0: the embedding rows)
         TRY(dbg_copy(l == 0 ? FFMI_DBG_EMBED : FFMI_DBG_HIDDEN, l == 0 ? 0 : l - 1, res, T));
@@ -681,11 +695,13 @@ struct LlamaGPU : public ffmi_model {
       FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
                                  &qkv_part));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
+      mk();
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_QKV, l, qkv, qkv_part, T));
       pr = prof_begin(on);
       TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s,
                              mode == FFMI_MODEL_TREE ? tree_parity : -1));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
+      mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_ATTN_OUT, l, att, T));
       ffmi::Partials o_part;
       if (o.tp_size == 1) {
@@ -693,31 +709,38 @@ struct LlamaGPU : public ffmi_model {
         FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
                                    H <= 8192 ? &o_part : nullptr));
         prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+        mk();
       } else {  // GEMM + all-reduce (overlapped over xGMI): timed together
         pr = prof_begin(on);
         TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+        mk();
       }
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_O_PROJ, l, proj, o_part, T));
       pr = prof_begin(on);
       FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
                                     o_part));
       prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+      mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_FFN_NORM, l, h, T));
       pr = prof_begin(on);
       const int YP = packed ? FFMI_Y_PACKED : 0;
       TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
+      mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_MLP_ACT, l, mlp, T));
       if (o.tp_size == 1) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
                                    H <= 8192 ? &down_part : nullptr));
         prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+        mk();
+        mk();  // (two back to back: the marker-to-marker boundary itself)
       } else {
         pr = prof_begin(on);
         TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+        mk();
       }
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_DOWN, l, proj, down_part, T));
     }

@@ -185,6 +185,7 @@ SIGNATURES = {
     "ffmi_pack_activations": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_debug_gemm_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
     "ffmi_debug_attn_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
+    "ffmi_debug_markers": (ctypes.c_long, [c_void_p, ctypes.c_long]),
 }
 
 # test doubles: libffmi_testmodel.so (include/ffmi_test.h), never the product

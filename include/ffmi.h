@@ -451,6 +451,9 @@ long ffmi_debug_gemm_stamps(long long *dst, long max_waves);
  * the commits, after the KV update, after its barrier, after the V^T stores
  * [100 MHz]; HW_ID, chunks). */
 long ffmi_debug_attn_stamps(long long *dst, long max_waves);
+/* FFMI_MARKERS=1 diagnostics: realtime-clock markers (100 MHz) enqueued
+ * between the kernels of the model's last layer; copies up to n (<= 64). */
+long ffmi_debug_markers(long long *dst, long n);
 
 const char *ffmi_status_str(ffmi_status s);
 /* message + file:line of the last failing check on this process */

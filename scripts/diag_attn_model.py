@@ -23,7 +23,12 @@ def main():
     ap.add_argument("--layers", type=int, default=4)
     ap.add_argument("--decode", type=int, default=32)
     ap.add_argument("--mode", default="spec", choices=["spec", "incr"])
+    ap.add_argument("--ssm", action="store_true",
+                    help="stamp the 68M SSM's d = 64 beam-step attention instead (FFMI_ATTN_STAMP=64)")
     args = ap.parse_args()
+    if args.ssm:
+        os.environ["FFMI_ATTN_STAMP"] = "64"
+        assert args.mode == "spec"
     bench.fa = fa
     cfg = dict(bench.LLAMA_7B, num_layers=args.layers)
     B, P = 8, 128
@@ -40,7 +45,7 @@ def main():
         rm.register_ssm_model(ssm)
     fa.generate(rm, llm, prompts, max_length=P + args.decode, spec=spec)
     L = fa.ffmi.lib()
-    buf = np.zeros((B * 32 * 8, 12), np.int64)
+    buf = np.zeros((B * (12 if args.ssm else 32) * 8, 12), np.int64)
     m = L.ffmi_debug_attn_stamps(buf.ctypes.data, buf.shape[0])
     st = buf[:m]
     t0 = st[:, 0].min()
