@@ -734,7 +734,8 @@ extern "C" ffmi_status ffmi_comm_peer_export(ffmi_comm *c, size_t max_bytes, voi
 }
 
 static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows, size_t cols,
-                            size_t ld, size_t col0, int dtype, hipStream_t s) {
+                            size_t ld, size_t col0, int dtype, hipStream_t s,
+                            const ffmi::Partials *slabs = nullptr) {
   PeerState &p = *c->peer;
   const size_t esz = dtype == FFMI_F16 ? 2 : 4;
   const size_t bytes = rows * cols * esz;
@@ -742,6 +743,10 @@ static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows
   FFMI_CHECK((cols * esz) % 16 == 0 && ((size_t)in & 15) == 0 && ((size_t)out & 15) == 0 &&
                  (ld * esz) % 16 == 0 && (col0 * esz) % 16 == 0,
              FFMI_ERR_UNSUPPORTED);
+  if (slabs && slabs->S > 0)
+    FFMI_CHECK(dtype == FFMI_F16 && slabs->S <= 8 && slabs->NP >= (int)cols && slabs->NP % 4 == 0 &&
+                   ((size_t)slabs->p & 15) == 0,
+               FFMI_ERR_UNSUPPORTED);
   ffmi::PeerArgs a;
   for (int r = 0; r < ffmi::kMaxPeers; ++r) a.base[r] = p.base[r];
   a.nranks = c->nranks;
@@ -757,6 +762,7 @@ static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows
   a.esz = esz;
   a.err = p.err_d;
   a.timeout_ticks = p.timeout_ticks;
+  if (slabs && slabs->S > 0) a.slabs = slabs->p, a.S = slabs->S, a.NP = slabs->NP, a.rows = rows;
   FFMI_HIP(ffmi::launch_peer_allreduce(a, bytes >= p.two_shot_min, s));
   return FFMI_OK;
 }
@@ -851,8 +857,8 @@ bool comm_peer_attached(const ffmi_comm *c) { return c && c->peer && c->peer->at
 bool comm_has_fallback(const ffmi_comm *c) { return c && (c->comm || c->local); }
 bool comm_is_rccl(const ffmi_comm *c) { return c && c->comm && !c->local; }
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
-                                int ld, int col0, int dtype, hipStream_t s) {
-  return peer_run(c, in, out, rows, cols, ld, col0, dtype, s);
+                                int ld, int col0, int dtype, hipStream_t s, const Partials *slabs) {
+  return peer_run(c, in, out, rows, cols, ld, col0, dtype, s, slabs);
 }
 ffmi_status comm_status(ffmi_comm *c) {
   return c && c->peer && c->peer->attached ? ffmi_comm_peer_status(c) : FFMI_OK;

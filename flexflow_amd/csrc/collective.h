@@ -36,6 +36,12 @@ struct PeerArgs {
   size_t esz;
   int *err;               // host-mapped error word (0 = ok)
   uint64_t timeout_ticks;  // s_memrealtime ticks (100 MHz)
+  // split-K input (f16 only): `in` unused, this rank's partial is the sum of
+  // S fp32 slabs [S][rows][NP] in slab order, rounded once to fp16 -- the
+  // value the GEMM's reduce pass would have written, folded into the copy-in
+  const float *slabs = nullptr;
+  int S = 0;
+  size_t NP = 0, rows = 0;
 };
 
 hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s);

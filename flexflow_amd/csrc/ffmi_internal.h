@@ -229,9 +229,12 @@ bool comm_has_fallback(const ffmi_comm *c);
 // an RCCL communicator (stream-capturable all-reduce)
 bool comm_is_rccl(const ffmi_comm *c);
 // sum of every rank's [rows][cols] `in` into `out` (row stride ld, starting
-// at column col0) over the xGMI transport
+// at column col0) over the xGMI transport; with `slabs` (f16 only) this
+// rank's partial is the sum of the GEMM's deferred split-K slabs instead of
+// `in` (the reduce pass folded into the copy-in)
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
-                                int ld, int col0, int dtype, hipStream_t s);
+                                int ld, int col0, int dtype, hipStream_t s,
+                                const Partials *slabs = nullptr);
 // FFMI_OK, or the transport's timeout error after a synchronised step
 ffmi_status comm_status(ffmi_comm *c);
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,

@@ -826,8 +826,11 @@ static bool g_attn_stamp_gate = true;
 void attn_stamp_gate(bool open) { g_attn_stamp_gate = open; }
 static long long *attn_stamp_buf(int wgs) {
   static const bool on = getenv("FFMI_ATTN_STAMP") != nullptr;
-  if (!on || !g_attn_stamp_gate) return nullptr;
+  if (!on) return nullptr;
+  // (allocated on the first launch, gate open or not: a later first use may
+  // sit inside a graph capture, where hipMalloc fails)
   if (!g_attn_stamps && hipMalloc(&g_attn_stamps, (size_t)8 << 20) != hipSuccess) return nullptr;
+  if (!g_attn_stamp_gate) return nullptr;
   g_attn_stamp_waves = std::min<long>((long)wgs * 8, ((long)8 << 20) / 96);
   return g_attn_stamps;
 }

@@ -140,7 +140,32 @@ __device__ __forceinline__ uint4 *out_vec(const PeerArgs &a, size_t v) {
                                    ((row * a.ld + a.col0 + col) * a.esz));
 }
 
-template <int DT, bool TWO_SHOT>
+// copy-in of a split-K partial: the 8 fp16 outputs of vector v, every slab
+// load issued before the first add (MAXS >= S; indices past S re-read the
+// last slab and are not added), summed in slab order and rounded once
+template <int MAXS>
+__device__ __forceinline__ uint4 slab_vec(const PeerArgs &a, size_t v) {
+  const size_t e = v * 8, row = e / a.cols, col = e % a.cols;
+  const float *q = a.slabs + row * a.NP + col;
+  const size_t slab = a.rows * a.NP;
+  f4 lo[MAXS], hi[MAXS];
+#pragma unroll
+  for (int s = 0; s < MAXS; ++s) {
+    const float *qs = q + (size_t)min(s, a.S - 1) * slab;
+    lo[s] = *reinterpret_cast<const f4 *>(qs);
+    hi[s] = *reinterpret_cast<const f4 *>(qs + 4);
+  }
+  f4 l = lo[0], h = hi[0];
+#pragma unroll
+  for (int s = 1; s < MAXS; ++s)
+    if (s < a.S) l += lo[s], h += hi[s];
+  h8 o;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = (_Float16)l[i], o[i + 4] = (_Float16)h[i];
+  return __builtin_bit_cast(uint4, o);
+}
+
+template <int DT, bool TWO_SHOT, int MAXS = 0>
 __global__ __launch_bounds__(kThreads) void peer_allreduce_kernel(PeerArgs a) {
   char *own = a.base[a.rank];
   unsigned *hdr = reinterpret_cast<unsigned *>(own + kHdrCounters);
@@ -152,11 +177,15 @@ __global__ __launch_bounds__(kThreads) void peer_allreduce_kernel(PeerArgs a) {
   const size_t stride = (size_t)G * kThreads;
   const size_t tid0 = (size_t)blockIdx.x * kThreads + threadIdx.x;
 
-  // 1. copy-in
+  // 1. copy-in (MAXS > 0: the sum of the GEMM's split-K slabs)
   {
-    const uint4 *src = reinterpret_cast<const uint4 *>(a.in);
     uint4 *dst = reinterpret_cast<uint4 *>(own + in_off);
-    for (size_t v = tid0; v < a.nvec; v += stride) dst[v] = src[v];
+    if constexpr (MAXS > 0) {
+      for (size_t v = tid0; v < a.nvec; v += stride) dst[v] = slab_vec<MAXS>(a, v);
+    } else {
+      const uint4 *src = reinterpret_cast<const uint4 *>(a.in);
+      for (size_t v = tid0; v < a.nvec; v += stride) dst[v] = src[v];
+    }
   }
   // 2. signal
   if (arrive_last(&hdr[kCnt0], G) && threadIdx.x == 0) push_flags(a, kInbox0, e);
@@ -206,7 +235,22 @@ hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s
   size_t per = two_shot ? (a.nvec + a.nranks - 1) / a.nranks : a.nvec;
   unsigned G = (unsigned)std::min<size_t>(kMaxPeerBlocks, (per + kThreads - 1) / kThreads);
   if (G == 0) G = 1;
-  if (a.esz == 2) {
+  if (a.slabs) {
+    if (a.esz != 2 || a.S < 1 || a.S > 8) return hipErrorInvalidValue;
+    const int ms = a.S <= 2 ? 2 : a.S <= 4 ? 4 : 8;
+#define FFMI_PEER_SL(TS, MS) \
+  hipLaunchKernelGGL((peer_allreduce_kernel<0, TS, MS>), dim3(G), dim3(kThreads), 0, s, a)
+    if (two_shot) {
+      if (ms == 2) FFMI_PEER_SL(true, 2);
+      else if (ms == 4) FFMI_PEER_SL(true, 4);
+      else FFMI_PEER_SL(true, 8);
+    } else {
+      if (ms == 2) FFMI_PEER_SL(false, 2);
+      else if (ms == 4) FFMI_PEER_SL(false, 4);
+      else FFMI_PEER_SL(false, 8);
+    }
+#undef FFMI_PEER_SL
+  } else if (a.esz == 2) {
     if (two_shot) hipLaunchKernelGGL((peer_allreduce_kernel<0, true>), dim3(G), dim3(kThreads), 0, s, a);
     else hipLaunchKernelGGL((peer_allreduce_kernel<0, false>), dim3(G), dim3(kThreads), 0, s, a);
   } else {

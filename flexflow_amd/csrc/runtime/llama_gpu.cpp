@@ -69,6 +69,7 @@ struct LlamaGPU : public ffmi_model {
   // (ncclAllReduce is stream-capturable); an in-process local group is not
   // (its all-reduce synchronises the host) and runs eager and unsplit
   bool rccl = false;
+  bool solo = false;  // TP shard over a 1-rank communicator without transport or RCCL
   int tp_chunks = 1;
   hipStream_t comm_stream = nullptr;
   uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
@@ -76,6 +77,7 @@ struct LlamaGPU : public ffmi_model {
   hipEvent_t ev_comm_done = nullptr;
   float *ws = nullptr;  // split-K workspace of the GEMMs
   size_t ws_bytes = 0;
+  size_t ws_chunk = 0;  // per-chunk workspace of the overlapped row-parallel GEMMs
   int32_t *ids_h = nullptr;
   bool result_copy = getenv("FFMI_RESULT_COPY") && atoi(getenv("FFMI_RESULT_COPY")) != 0;
   float *probs_h = nullptr;
@@ -395,6 +397,10 @@ struct LlamaGPU : public ffmi_model {
       return FFMI_ERR_INVALID;
     }
     rccl = P > 1 && !peer && ffmi::comm_is_rccl(o.comm);
+    // a shard over a one-rank communicator with no RCCL state (the per-rank
+    // shard bench): every all-reduce is the identity, so o/down defer their
+    // slabs to the residual norm exactly as at TP = 1
+    solo = P > 1 && !peer && !rccl && ffmi::comm_size(o.comm) == 1;
     if (peer || rccl) {
       tp_chunks = 2;
       if (const char *e = getenv("FFMI_TP_OVERLAP")) tp_chunks = atoi(e) ? 2 : 1;
@@ -415,6 +421,17 @@ struct LlamaGPU : public ffmi_model {
         const size_t w4 = ffmi_linear_workspace_bytes(t, H, Fl, FFMI_EPI_NONE);
         const size_t w5 = ffmi_linear_workspace_bytes(t, Vl, H, FFMI_EPI_NONE);
         ws_bytes = std::max(ws_bytes, std::max(std::max(std::max(w1, w2), std::max(w3, w4)), w5));
+      }
+      // the row-parallel column chunks over the xGMI transport defer their
+      // split-K slabs to the all-reduce's copy-in on comm_stream while the
+      // next chunk computes: one workspace region per chunk
+      if (peer && tp_chunks > 1) {
+        const int Hc = H / tp_chunks;
+        for (int t = 16; t <= Tm; t += 16)
+          ws_chunk = std::max(ws_chunk, std::max(ffmi_linear_workspace_bytes(t, Hc, Hl, FFMI_EPI_NONE),
+                                                 ffmi_linear_workspace_bytes(t, Hc, Fl, FFMI_EPI_NONE)));
+        ws_chunk = (ws_chunk + 255) & ~(size_t)255;
+        ws_bytes = std::max(ws_bytes, ws_chunk * tp_chunks);
       }
       if (ws_bytes) TRY(alloc(&ws, (ws_bytes + 3) / 4));
     }
@@ -524,8 +541,12 @@ struct LlamaGPU : public ffmi_model {
                                     int T, int XP) {
     const int H = c.hidden;
     if (!(peer || rccl) || tp_chunks == 1) {
-      FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream, nullptr));
-      if (peer) return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream);
+      // over the transport the split-K reduce is the all-reduce's copy-in
+      ffmi::Partials part;
+      FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream, peer ? &part : nullptr));
+      if (peer)
+        return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream,
+                                         part.S > 0 ? &part : nullptr);
       return allreduce(out, (size_t)T * H);
     }
     const int Hc = H / tp_chunks;
@@ -533,13 +554,18 @@ struct LlamaGPU : public ffmi_model {
     const size_t tiles = (size_t)(Hc / 16) * ffmi::w_tile_stride((K + 31) / 32);
     for (int ch = 0; ch < tp_chunks; ++ch) {
       uint16_t *cb = chunk_buf + (size_t)ch * T * Hc;
-      FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb, ws, ws_bytes, T, Hc, K, XP, stream,
-                                 nullptr, H / 16));
+      // over the transport: the chunk's split-K slabs (own workspace region)
+      // go to the all-reduce's copy-in, no reduce pass on this stream
+      ffmi::Partials part;
+      FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb,
+                                 peer ? (float *)((char *)ws + ch * ws_chunk) : ws,
+                                 peer ? ws_chunk : ws_bytes, T, Hc, K, XP, stream,
+                                 peer ? &part : nullptr, H / 16));
       FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
       FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
       if (peer) {  // the transport reduces straight into out's columns
-        ffmi_status st =
-            ffmi::comm_allreduce_cols(o.comm, cb, out, T, Hc, H, ch * Hc, FFMI_F16, comm_stream);
+        ffmi_status st = ffmi::comm_allreduce_cols(o.comm, cb, out, T, Hc, H, ch * Hc, FFMI_F16,
+                                                   comm_stream, part.S > 0 ? &part : nullptr);
         if (st != FFMI_OK) return st;
       } else {  // RCCL: contiguous in place, then into out's columns
         ffmi_status st = ffmi_allreduce(o.comm, cb, cb, (size_t)T * Hc, FFMI_F16,
@@ -668,6 +694,8 @@ struct LlamaGPU : public ffmi_model {
       auto mk = [&]() {
         if (mark_on) (void)ffmi::launch_marker(mark_i++, stream);
       };
+      // (the marker buffer is allocated by an eager launch, never in a capture)
+      if (marker_h && l == 0 && record_upload) (void)ffmi::launch_marker(63, stream);
       mk();
       pr = prof_begin(on);
       // split-K GEMMs leave their partial slabs for the next kernel to combine
@@ -704,7 +732,7 @@ struct LlamaGPU : public ffmi_model {
       mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_ATTN_OUT, l, att, T));
       ffmi::Partials o_part;
-      if (o.tp_size == 1) {
+      if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
                                    H <= 8192 ? &o_part : nullptr));
@@ -729,7 +757,7 @@ struct LlamaGPU : public ffmi_model {
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_MLP_ACT, l, mlp, T));
-      if (o.tp_size == 1) {
+      if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
                                    H <= 8192 ? &down_part : nullptr));

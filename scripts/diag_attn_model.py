@@ -14,6 +14,10 @@ import numpy as np
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 os.environ.setdefault("FFMI_ATTN_STAMP", "1")
+# stamp the last layer of the last FULL step only (T = 168 verify, 8 x 21 tree
+# tokens; the last steps of a generate are shorter): FFMI_MARKERS gates it
+os.environ.setdefault("FFMI_MARKERS", "4096")
+os.environ.setdefault("FFMI_MARKERS_T", "168")
 import bench  # noqa: E402
 import flexflow_amd as fa  # noqa: E402
 
@@ -26,8 +30,11 @@ def main():
     ap.add_argument("--ssm", action="store_true",
                     help="stamp the 68M SSM's d = 64 beam-step attention instead (FFMI_ATTN_STAMP=64)")
     args = ap.parse_args()
+    if args.mode == "incr":
+        os.environ["FFMI_MARKERS_T"] = "8"  # a full decode batch
     if args.ssm:
         os.environ["FFMI_ATTN_STAMP"] = "64"
+        os.environ["FFMI_MARKERS"] = "0"  # (the SSM: its last launch)
         assert args.mode == "spec"
     bench.fa = fa
     cfg = dict(bench.LLAMA_7B, num_layers=args.layers)
