@@ -422,8 +422,15 @@ def main():
     # FFMI_PEER_TIMEOUT_S for a peer, and loading skew must not eat into that
     device_sync()
     ctrl.barrier()
-    for _ in range(args.warmup):
+
+    def progress(msg):  # rank 0, stderr: a long run (N ranks) stays visibly alive
+        if rank == 0:
+            print(f"[bench] {msg} ({time.time() - t_init:.1f} s)", file=sys.stderr, flush=True)
+
+    progress("models built")
+    for i in range(args.warmup):
         run_generate(rm, llm, prompts, max_len, spec)
+        progress(f"warmup {i + 1}/{args.warmup}")
     if args.profile:
         llm.set_profiling(args.profile)
     ctrl.barrier()
@@ -444,6 +451,7 @@ def main():
         llm_us += st.llm_us
         ssm_us += st.ssm_us
         wall_us += st.wall_us
+        progress(f"step {_ + 1}/{args.steps}")
     device_sync()
     ctrl.barrier()
     elapsed = ctrl.max(time.time() - t0)

@@ -78,6 +78,9 @@ struct LlamaGPU : public ffmi_model {
   float *ws = nullptr;  // split-K workspace of the GEMMs
   size_t ws_bytes = 0;
   size_t ws_chunk = 0;  // per-chunk workspace of the overlapped row-parallel GEMMs
+  // split-K slabs summed by the all-reduce's copy-in (FFMI_AR_SLABS=0: the
+  // GEMM's own reduce pass, A/B runs)
+  bool ar_slabs = !getenv("FFMI_AR_SLABS") || atoi(getenv("FFMI_AR_SLABS")) != 0;
   int32_t *ids_h = nullptr;
   bool result_copy = getenv("FFMI_RESULT_COPY") && atoi(getenv("FFMI_RESULT_COPY")) != 0;
   float *probs_h = nullptr;
@@ -425,7 +428,7 @@ struct LlamaGPU : public ffmi_model {
       // the row-parallel column chunks over the xGMI transport defer their
       // split-K slabs to the all-reduce's copy-in on comm_stream while the
       // next chunk computes: one workspace region per chunk
-      if (peer && tp_chunks > 1) {
+      if (peer && ar_slabs && tp_chunks > 1) {
         const int Hc = H / tp_chunks;
         for (int t = 16; t <= Tm; t += 16)
           ws_chunk = std::max(ws_chunk, std::max(ffmi_linear_workspace_bytes(t, Hc, Hl, FFMI_EPI_NONE),
@@ -543,7 +546,8 @@ struct LlamaGPU : public ffmi_model {
     if (!(peer || rccl) || tp_chunks == 1) {
       // over the transport the split-K reduce is the all-reduce's copy-in
       ffmi::Partials part;
-      FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream, peer ? &part : nullptr));
+      FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream,
+                                 peer && ar_slabs ? &part : nullptr));
       if (peer)
         return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream,
                                          part.S > 0 ? &part : nullptr);
@@ -557,10 +561,11 @@ struct LlamaGPU : public ffmi_model {
       // over the transport: the chunk's split-K slabs (own workspace region)
       // go to the all-reduce's copy-in, no reduce pass on this stream
       ffmi::Partials part;
+      const bool def = peer && ar_slabs;
       FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb,
-                                 peer ? (float *)((char *)ws + ch * ws_chunk) : ws,
-                                 peer ? ws_chunk : ws_bytes, T, Hc, K, XP, stream,
-                                 peer ? &part : nullptr, H / 16));
+                                 def ? (float *)((char *)ws + ch * ws_chunk) : ws,
+                                 def ? ws_chunk : ws_bytes, T, Hc, K, XP, stream,
+                                 def ? &part : nullptr, H / 16));
       FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
       FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
       if (peer) {  // the transport reduces straight into out's columns
