@@ -296,3 +296,21 @@ def test_result_copy_modes_same_tokens(monkeypatch, graphs):
     assert out[0] == out[1]
     assert out[0][0] == out[0][1]  # and SpecInfer == incremental decoding
 
+
+
+@pytest.mark.parametrize("graphs", [True, False])
+def test_blob_fetch_same_tokens(monkeypatch, graphs):
+    """The step's metadata blob read by the first kernel straight from the
+    mapped pinned staging (default; it also copies the blob to the device for
+    the later kernels) vs a separate H2D copy (FFMI_BLOB_FETCH=0): identical
+    tokens, graphed and eager, incremental decoding and SpecInfer."""
+    ps = prompts(4, 1000, 5, 40, 14)
+    if not graphs:
+        monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
+    out = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("FFMI_BLOB_FETCH", mode)
+        inc, _ = run_incr(ps, 60)
+        spec, _ = run_spec(ps, 60, SSM_CFG, 5)
+        out.append(([r.output_tokens for r in inc], [r.output_tokens for r in spec]))
+    assert out[0] == out[1]

@@ -63,10 +63,14 @@ def test_vocab_shard_topk_matches_unsharded(n, T, V, k):
 
 
 CFG4V = dict(CFG4, vocab_size=1024)  # V/TP a multiple of 16: lm_head vocab-sharded
+# a long down projection (K = F/TP = 2048): its row-parallel GEMM splits K
+# (8 slabs) and the all-reduce's copy-in sums the slabs
+CFG4F = dict(CFG4, intermediate=4096)
 
 
 @pytest.mark.parametrize("tp,overlap,cfg", [(2, "1", CFG4), (2, "0", CFG4), (4, "1", CFG4),
-                                            (2, "1", CFG4V), (4, "1", CFG4V)])
+                                            (2, "1", CFG4V), (4, "1", CFG4V), (2, "1", CFG4F),
+                                            (2, "0", CFG4F)])
 def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
     """TP shards as separate processes over the xGMI transport (row-parallel
     GEMMs in two column halves, each all-reduced on a second stream while the
