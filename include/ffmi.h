@@ -304,7 +304,13 @@ typedef enum {
 typedef struct {
   int mode;                  /* ffmi_model_mode                                */
   int tp_rank, tp_size;      /* tensor parallelism (heads / FFN columns)       */
-  ffmi_comm *comm;           /* RCCL communicator (NULL when tp_size == 1)      */
+  ffmi_comm *comm;           /* communicator of tp_size ranks: RCCL, xGMI
+                              * transport or local group (NULL when tp_size == 1).
+                              * A ONE-rank communicator without RCCL state or
+                              * transport with tp_size > 1 runs shard tp_rank
+                              * alone, every all-reduce the identity: the
+                              * per-rank compute measurement of
+                              * scripts/tp_shard_bench.py (tokens meaningless) */
   int max_requests;          /* max_requests_per_batch                         */
   int max_tokens;            /* max tokens per batch (verify capacity for TREE) */
   int max_seq_len;           /* max_sequence_length                            */
