@@ -794,6 +794,17 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
     }
   }
+  // prefill blocks (>= 4 row blocks: T > 576 at MTW = 3): the k-step model
+  // above is calibrated at T = 168; forced-plan sweeps at T = 1024
+  // (scripts/gpu_prefill_plans.sh, LLaMA-7B shapes) put 8 tiles unsplit
+  // first on qkv / o / gate-up / lm_head and 8 tiles x 2 slices on the
+  // K = 11008 down projection (gate/up 337 -> 270 us, qkv 149 -> 139,
+  // down 148 -> 135, lm_head 428 -> 409); FFMI_PREFILL_PLAN=0 keeps the model
+  static const bool prefill_plan = !getenv("FFMI_PREFILL_PLAN") || atoi(getenv("FFMI_PREFILL_PLAN")) != 0;
+  if (prefill_plan && p.mblocks >= 4) {
+    p.NTW = 8;
+    p.S = K >= 8192 && KT >= 2 ? 2 : 1;
+  }
   // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split of
   // every M-split launch; "N:K:NTW,S;..." only of the listed shapes
   static const char *force = getenv("FFMI_GEMM_PLAN");
