@@ -146,9 +146,28 @@ hipError_t launch_pack_weight(const uint16_t *src, int ld, int row0, int col0,
 // Y is written and defer->S = 0.  Only for FFMI_EPI_NONE.  wpitch: tiles per
 // k-row of Wp's allocation (0 = the GEMM's own tile count; a column chunk of a
 // wider matrix passes the full matrix's).
+// Residual RMSNorm folded into the skinny GEMMs (T <= 32, unsplit), the
+// reference's ResidualRMSNorm (residual_rms_norm_kernels.cu:98-131) split
+// over the two GEMMs around it:
+//  * producer (o / down projection, EPI 0): Y = half(res_in + half(X.W^T))
+//    (Y may alias res_in) and, per row and 16-column tile, the fp32 sum of
+//    squares of those fp16 values -> ss_out[T][N/16];
+//  * consumer (the next qkv or gate/up): X is that residual, row-major; the
+//    prologue turns the row's ss_in partials into rms = half(1/sqrt(sum/K +
+//    eps)) and every X fragment becomes half(half(x * rms) * w[k]) before its
+//    MFMA -- the norm kernel's arithmetic, fp16 multiplies.
+struct FuseArgs {
+  int kind = 0;                     // 0 none, 1 producer, 2 consumer
+  const uint16_t *res_in = nullptr;  // producer: [T][N] residual
+  float *ss_out = nullptr;          // producer: [T][N/16]
+  const float *ss_in = nullptr;     // consumer: [T][nss]
+  int nss = 0;                      // consumer: partials per row (= K/16)
+  const uint16_t *wnorm = nullptr;  // consumer: norm weight [K]
+  float eps = 0.f;
+};
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
-                       Partials *defer = nullptr, int wpitch = 0);
+                       Partials *defer = nullptr, int wpitch = 0, const FuseArgs *fuse = nullptr);
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue);
 // fp16 Y[T][N] (row-major) of deferred split-K slabs, summed in slab order and
 // rounded once: the value every consumer of the slabs computes (tensor capture)

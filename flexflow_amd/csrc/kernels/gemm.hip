@@ -58,14 +58,106 @@ __device__ __forceinline__ uint16_t silu_mul_h(float gacc, float uacc) {
 // workgroup reduces its K slice over its waves and writes an fp32 partial
 // slab [S][T][NTILES*16] that the consumer combines in slice order
 // (Partials, the M-split kernel's slab layout).
-template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false, bool NTL = false>
+// v of the lane n places further up the same 16-lane DPP row (row_ror:n)
+template <int NR>
+__device__ __forceinline__ float row_ror_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               0x120 + NR, 0xf, 0xf, false));
+}
+
+// v of lane l (wave-uniform result), bit-exact
+__device__ __forceinline__ float lane_f(float v, int l) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+
+// FZ (FuseArgs, ffmi_internal.h): 1 = residual-add producer epilogue (EPI 0,
+// unsplit), 2 = RMSNorm consumer prologue on row-major X.
+template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false, bool NTL = false, int FZ = 0>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
-    int NTILES, int xp, int yp, size_t wts, size_t wks) {
+    uint16_t *Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
+    int NTILES, int xp, int yp, size_t wts, size_t wks, FuseArgs fz) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
   const int wave = threadIdx.x >> 6;
+  // FZ == 1: the residual this wave-0 epilogue adds, loaded up front
+  _Float16 rpre[FZ == 1 ? MT : 1][FZ == 1 ? NT : 1][4];
+  if constexpr (FZ == 1) {
+    if (wave == 0) {
+#pragma unroll
+      for (int j = 0; j < NT; ++j) {
+        const int n = min((int)(blockIdx.x * NT + j) * 16 + (lane & 15), N - 1);
+#pragma unroll
+        for (int i = 0; i < MT; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = min(i * 16 + (lane >> 4) * 4 + r, T - 1);
+            rpre[i][j][r] = reinterpret_cast<const _Float16 *>(fz.res_in)[(size_t)m * N + n];
+          }
+      }
+    }
+  }
+  // FZ == 2: rms of every row (the norm kernel's arithmetic on the
+  // producer's per-tile sums of squares, summed in a fixed order), then the
+  // rms of this lane's rows as an fp16 multiplier of its X fragments
+  h8 rms8[FZ == 2 ? MT : 1];
+  // wave w owns rows w, w + KW, ... (<= RPW of them); lane l sums partials
+  // l, l + 64, ... (<= 4: nss <= 256) of each.  The loads go out first; the
+  // sums, the LDS exchange and its barrier (rms_finish) run once the wave's
+  // first batch of weight / X loads is in flight too (loads retire in order,
+  // so waiting for these does not wait for those): the two round trips
+  // overlap instead of adding up.  Every wave calls rms_finish exactly once.
+  constexpr int RPW = (MT * 16 + KW - 1) / KW;
+  __shared__ float sRms[FZ == 2 ? MT * 16 : 1];
+  float pv[FZ == 2 ? RPW : 1][4];
+  bool rdone = FZ != 2;
+  if constexpr (FZ == 2) {
+#pragma unroll
+    for (int rr = 0; rr < RPW; ++rr) {
+      const int m = min(wave + rr * KW, T - 1);
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        pv[rr][c] = fz.ss_in[(size_t)m * fz.nss + min(lane + 64 * c, fz.nss - 1)];
+    }
+  }
+  auto rms_finish = [&]() {
+    if constexpr (FZ == 2) {
+      if (rdone) return;
+      rdone = true;
+#pragma unroll
+      for (int rr = 0; rr < RPW; ++rr) {
+        const int m = wave + rr * KW;
+        float v = 0.f;
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          if (lane + 64 * c < fz.nss) v += pv[rr][c];
+        // 16-lane DPP rows, then the four row sums in row order
+        v += row_ror_f<1>(v);
+        v += row_ror_f<2>(v);
+        v += row_ror_f<4>(v);
+        v += row_ror_f<8>(v);
+        v = ((lane_f(v, 0) + lane_f(v, 16)) + lane_f(v, 32)) + lane_f(v, 48);
+        if (lane == 0 && m < T) {
+          const float rf = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(v, (float)K), fz.eps)));
+          sRms[m] = __half2float(__float2half_rn(rf));
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < MT; ++i) {
+        const _Float16 r = (_Float16)sRms[min(i * 16 + (lane & 15), T - 1)];
+        rms8[i] = h8{r, r, r, r, r, r, r, r};
+      }
+    }
+  };
+  // norm weight fragment of k-step k (this lane's 8 columns)
+  auto ldwn = [&](int k) -> h8 {
+    return *reinterpret_cast<const h8 *>(fz.wnorm + (size_t)k * 32 + 8 * (lane >> 4));
+  };
+  // y = half(half(x * rms) * w): two fp16 multiplies, as the norm kernel
+  auto nrm = [&](h8 &a, int i, const h8 &w) {
+    if constexpr (FZ == 2) a = (a * rms8[i]) * w;
+  };
   const int cb = blockIdx.x, ks = blockIdx.y, S = gridDim.y;
   const int tile0 = cb * NT;
   const int m0 = 0;
@@ -110,19 +202,26 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const int nb = (ke - kt) / UP;
     if (nb > 0) {
       h8 bA[UP][NT], aA[UP][MT], bB[UP][NT], aB[UP][MT];
-      auto ld = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT], int k0) {
+      h8 wA[FZ == 2 ? UP : 1], wB[FZ == 2 ? UP : 1];
+      auto ld = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT], h8(&ww)[FZ == 2 ? UP : 1], int k0) {
 #pragma unroll
         for (int u = 0; u < UP; ++u)
 #pragma unroll
           for (int j = 0; j < NT; ++j)
             bb[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(k0 + u) * wks);
 #pragma unroll
-        for (int u = 0; u < UP; ++u)
+        for (int u = 0; u < UP; ++u) {
 #pragma unroll
           for (int i = 0; i < MT; ++i)
             aa[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)(k0 + u) * XS);
+          if constexpr (FZ == 2) ww[u] = ldwn(k0 + u);
+        }
       };
-      auto mm = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT]) {
+      auto mm = [&](h8(&bb)[UP][NT], h8(&aa)[UP][MT], h8(&ww)[FZ == 2 ? UP : 1]) {
+#pragma unroll
+        for (int u = 0; u < UP; ++u)
+#pragma unroll
+          for (int i = 0; i < MT; ++i) nrm(aa[u][i], i, ww[FZ == 2 ? u : 0]);
 #pragma unroll
         for (int u = 0; u < UP; ++u)
 #pragma unroll
@@ -132,29 +231,30 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
               acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(aa[u][i], bb[u][j], acc[i][j],
                                                                 0, 0, 0);
       };
-      ld(bA, aA, kt);
+      ld(bA, aA, wA, kt);
+      rms_finish();
       int q = 0;
       for (; q + 2 < nb; q += 2) {
-        ld(bB, aB, kt + UP);
+        ld(bB, aB, wB, kt + UP);
         __builtin_amdgcn_sched_barrier(0);
-        mm(bA, aA);
+        mm(bA, aA, wA);
         __builtin_amdgcn_sched_barrier(0);
-        ld(bA, aA, kt + 2 * UP);
+        ld(bA, aA, wA, kt + 2 * UP);
         __builtin_amdgcn_sched_barrier(0);
-        mm(bB, aB);
+        mm(bB, aB, wB);
         __builtin_amdgcn_sched_barrier(0);
         kt += 2 * UP;
       }
       if (q + 1 < nb) {  // two batches left
-        ld(bB, aB, kt + UP);
+        ld(bB, aB, wB, kt + UP);
         __builtin_amdgcn_sched_barrier(0);
-        mm(bA, aA);
+        mm(bA, aA, wA);
         __builtin_amdgcn_sched_barrier(0);
-        mm(bB, aB);
+        mm(bB, aB, wB);
         kt += 2 * UP;
       } else {  // one batch left
         __builtin_amdgcn_sched_barrier(0);
-        mm(bA, aA);
+        mm(bA, aA, wA);
         kt += UP;
       }
     }
@@ -162,20 +262,28 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
   for (; kt + U <= ke; kt += U) {
     h8 b[U][NT];
     h8 a[U][MT];
+    h8 wn[FZ == 2 ? U : 1];
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
       for (int j = 0; j < NT; ++j)
         b[u][j] = ld_weight<NTL>(wrow[j] + (size_t)(kt + u) * wks);
 #pragma unroll
-    for (int u = 0; u < U; ++u)
+    for (int u = 0; u < U; ++u) {
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)(kt + u) * XS);
+      if constexpr (FZ == 2) wn[u] = ldwn(kt + u);
+    }
+    rms_finish();
     // keep the whole batch of loads ahead of the MFMAs: left alone the
     // scheduler interleaves them and reuses registers, leaving ~7 loads in
     // flight per wave with a vmcnt wait before almost every MFMA
     __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) nrm(a[u][i], i, wn[FZ == 2 ? u : 0]);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -193,6 +301,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const int rem = ke - kt;
     h8 b[U - 1][NT];
     h8 a[U - 1][MT];
+    h8 wn[FZ == 2 ? U - 1 : 1];
 #pragma unroll
     for (int u = 0; u < U - 1; ++u) {
       const int kk = min(kt + u, ke - 1);
@@ -202,9 +311,15 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
 #pragma unroll
       for (int i = 0; i < MT; ++i)
         a[u][i] = *reinterpret_cast<const h8 *>(xrow[i] + (size_t)kk * XS);
+      if constexpr (FZ == 2) wn[u] = ldwn(kk);
     }
+    rms_finish();
     __builtin_amdgcn_sched_barrier(0);
     const h8 zero = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+#pragma unroll
+      for (int i = 0; i < MT; ++i) nrm(a[u][i], i, wn[FZ == 2 ? u : 0]);
 #pragma unroll
     for (int u = 0; u < U - 1; ++u) {
       if (u >= rem)
@@ -218,6 +333,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     }
   }
 
+  rms_finish();  // (a wave with an empty k-range still meets the barrier)
   // Cross-wave K reduction in a fixed order (wave 0 + 1 + ... + KW-1).
   if (KW > 1) {
     constexpr int REGS = MT * NT * 4;
@@ -260,6 +376,38 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     }
     return;
   }
+  if constexpr (FZ == 1) {
+    // residual add (the norm kernel's correctly rounded fp16 add of the
+    // rounded GEMM output), then per (row, tile) the sum of squares of the
+    // 16 new values: a fixed butterfly over the 16 lanes of the row
+#pragma unroll
+    for (int j = 0; j < NT; ++j) {
+      const int n = (tile0 + j) * 16 + (lane & 15);
+      const bool nok = tile0 + j < NTILES && n < N;
+#pragma unroll
+      for (int i = 0; i < MT; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          const _Float16 rh = rpre[i][j][r] + (_Float16)acc[i][j][r];
+          float sq = 0.f;
+          if (nok && m < T) {
+            reinterpret_cast<_Float16 *>(Y)[(size_t)m * N + n] = rh;
+            const float f = (float)rh;
+            sq = f * f;
+          }
+          // the 16 columns of the row are the 16 lanes of one DPP row:
+          // rotate-and-add within the row (VALU, no LDS crossbar)
+          sq += row_ror_f<1>(sq);
+          sq += row_ror_f<2>(sq);
+          sq += row_ror_f<4>(sq);
+          sq += row_ror_f<8>(sq);
+          if ((lane & 15) == 0 && m < T && tile0 + j < NTILES)
+            fz.ss_out[(size_t)m * NTILES + tile0 + j] = sq;
+        }
+    }
+    return;
+  }
   if (EPI == 0) {
 #pragma unroll
     for (int j = 0; j < NT; ++j) {
@@ -292,10 +440,10 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
   }
 }
 
-template <int MT, int NT, int KW, int U, int EPI>
+template <int MT, int NT, int KW, int U, int EPI, int FZ = 0>
 static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws, int T,
                       int N, int K, int KT, int NTILES, int S, hipStream_t s, int xp, int yp,
-                      bool nt, int wpitch) {
+                      bool nt, int wpitch, const FuseArgs &fz = FuseArgs()) {
   const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch);
   const int ncb = (NTILES + NT - 1) / NT;
   dim3 grid(ncb, S);
@@ -309,8 +457,8 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
   const int per_wave = ((KT + S - 1) / S + KW - 1) / KW;
   const bool pipe = force >= 0 ? force != 0 : per_wave >= 2 * U;
 #define FFMI_SKINNY_LAUNCH(PP, NL)                                                             \
-  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, PP, NL>), grid, dim3(KW * 64), lds, \
-                     s, X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp, wts, wks)
+  hipLaunchKernelGGL((gemm_skinny_kernel<MT, NT, KW, U, EPI, PP, NL, FZ>), grid, dim3(KW * 64), \
+                     lds, s, X, Wp, Y, ws, T, N, K, KT, NTILES, xp, yp, wts, wks, fz)
   if (pipe) {
     if (nt) FFMI_SKINNY_LAUNCH(true, true);
     else FFMI_SKINNY_LAUNCH(true, false);
@@ -422,6 +570,26 @@ static int skinny_split(int T, int N, int K, int epi, bool deferrable) {
   int S = 256 / ntiles;
   S = std::min(S, std::max(1, KT / 8));  // >= 1 k-step per wave of an 8-wave slice
   return std::max(1, std::min(S, 8));
+}
+
+// The fused residual/norm forms (FuseArgs; S == 1, T <= 32): the unfused
+// path's tile and wave choices, one instantiation set per role.
+template <int MT, int U, int FZ>
+static hipError_t dispatch_fused(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, int T, int N,
+                                 int K, int KT, int epi, hipStream_t s, int xp, int yp, bool nt,
+                                 int wpitch, const FuseArgs &fz) {
+  const int ntiles = (N + 15) / 16;
+  if (epi == FFMI_EPI_SILU_MUL) {
+    if constexpr (FZ == 2)
+      return run<MT, 2, 4, U, 1, 2>(X, Wp, Y, nullptr, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt,
+                                    wpitch, fz);
+    return hipErrorInvalidValue;
+  }
+  if (MT >= 2 && ntiles >= 512)
+    return run<MT, 2, 4, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
+  if (ntiles < 512 && KT >= 64 && !nt)
+    return run<MT, 1, 8, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
+  return run<MT, 1, 4, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
 }
 
 template <int MT, int U>
@@ -931,7 +1099,7 @@ hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, 
 
 hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
                        size_t ws_bytes, int T, int N, int K, int epilogue, hipStream_t s,
-                       Partials *defer, int wpitch) {
+                       Partials *defer, int wpitch, const FuseArgs *fuse) {
   if (defer) defer->S = 0;
   if (T <= 0) return hipSuccess;
   const int KT = K / 32;
@@ -941,6 +1109,25 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
   const bool nt = (epilogue & FFMI_W_STREAM) != 0;
   epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED | FFMI_W_STREAM);
   if ((xp && K % 32) || (yp && N % 32)) return hipErrorInvalidValue;
+  if (fuse && fuse->kind) {
+    // producer: row-major residual out, plain epilogue; consumer: row-major X
+    // (the residual), K = the norm width; both unsplit, T <= 32
+    if (mtiles > 2 || N % 16 || K % 32) return hipErrorInvalidValue;
+    if (fuse->kind == 1 && (epilogue || yp || !fuse->res_in || !fuse->ss_out))
+      return hipErrorInvalidValue;
+    if (fuse->kind == 2 && (xp || !fuse->ss_in || !fuse->wnorm || fuse->nss <= 0 || fuse->nss > 256))
+      return hipErrorInvalidValue;
+    const int wp = wpitch ? wpitch : (epilogue == FFMI_EPI_SILU_MUL ? 2 : 1) * ((N + 15) / 16);
+#define FFMI_FZ(MTV, FZV) \
+  return dispatch_fused<MTV, 8, FZV>(X, Wp, Y, T, N, K, KT, epilogue, s, xp, yp, nt, wp, *fuse)
+    if (mtiles <= 1) {
+      if (fuse->kind == 1) FFMI_FZ(1, 1);
+      FFMI_FZ(1, 2);
+    }
+    if (fuse->kind == 1) FFMI_FZ(2, 1);
+    FFMI_FZ(2, 2);
+#undef FFMI_FZ
+  }
   if (mtiles > 4) {
     const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);
 #define FFMI_RUN(M, NW) \

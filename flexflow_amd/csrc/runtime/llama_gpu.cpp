@@ -70,6 +70,15 @@ struct LlamaGPU : public ffmi_model {
   // (its all-reduce synchronises the host) and runs eager and unsplit
   bool rccl = false;
   bool solo = false;  // TP shard over a 1-rank communicator without transport or RCCL
+  // residual norms folded into the skinny GEMMs around them (T <= 32, TP = 1):
+  // per-tile sums of squares of the residual after o (ss_o) and after down
+  // (ss_d), [32][H/16] each.  Only where o/down run unsplit anyway (H/16 >=
+  // 128 tiles: LLaMA-7B decode, 2414 -> 2474-2488 tokens/s); the 68M SSM's
+  // o/down split K over workgroups, and unsplitting them to fuse cost more
+  // than the norm launches saved (SSM step +4 us).  FFMI_FUSE_NORM: 0 off,
+  // 1 auto (default), 2 every width (tests)
+  int fuse_norms = getenv("FFMI_FUSE_NORM") ? atoi(getenv("FFMI_FUSE_NORM")) : 1;
+  float *ss_o = nullptr, *ss_d = nullptr;
   int tp_chunks = 1;
   hipStream_t comm_stream = nullptr;
   uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
@@ -383,6 +392,8 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&qkv, (size_t)Tm * 3 * Hl));
     TRY(alloc(&att, (size_t)Tm * Hl));
     TRY(alloc(&proj, (size_t)Tm * H));
+    TRY(alloc(&ss_o, (size_t)2 * 32 * (H / 16)));
+    ss_d = ss_o + (size_t)32 * (H / 16);
     TRY(alloc(&mlp, (size_t)Tm * Fl));
     Vl = P > 1 && V % P == 0 && (V / P) % 16 == 0 ? V / P : V;
     if (const char *e = getenv("FFMI_VOCAB_SHARD"))  // A/B: 0 = replicated lm_head
@@ -691,6 +702,8 @@ struct LlamaGPU : public ffmi_model {
     static const int marker_h = getenv("FFMI_MARKERS") ? atoi(getenv("FFMI_MARKERS")) : 0;
     static const int marker_t = getenv("FFMI_MARKERS_T") ? atoi(getenv("FFMI_MARKERS_T")) : 0;
     int mark_i = 0;
+    const bool fuse = (fuse_norms == 2 || (fuse_norms == 1 && H >= 2048)) && !dbg &&
+                      o.tp_size == 1 && T <= 32 && H % 32 == 0 && Hl % 32 == 0 && H <= 4096;
     for (int l = 0; l < c.num_layers; ++l) {
       Layer &L = layers[l];
       const bool on = prof_on(l, T);
@@ -702,22 +715,39 @@ struct LlamaGPU : public ffmi_model {
       // (the marker buffer is allocated by an eager launch, never in a capture)
       if (marker_h && l == 0 && record_upload) (void)ffmi::launch_marker(63, stream);
       mk();
-      pr = prof_begin(on);
       // split-K GEMMs leave their partial slabs for the next kernel to combine
       // (rope-store for qkv; the residual norm for o/down when there is no
       // all-reduce in between) instead of a separate reduce pass
       const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
-      // layer 0: the embedding lookup gathers straight into the first norm
-      // (embedding_kernels.cu:233-244; res = the looked-up rows)
-      FFMI_HIP(ffmi::launch_rmsnorm(l == 0 ? embed : res, l == 0 ? nullptr : proj, L.in_norm, res,
-                                    h, T, H, eps, stream, packed,
-                                    l == 0 ? ffmi::Partials() : down_part,
-                                    l == 0 ? (blob_fetch ? batch->host : batch->dev) : nullptr,
-                                    l == 0 && blob_fetch ? batch->dev : nullptr, blob_bytes));
-      // the staging is free for the next step once the fetch has read it
-      if (l == 0 && blob_fetch && record_upload) FFMI_HIP(hipEventRecord(batch->uploaded, stream));
-      prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
-      mk();
+      // fused residual norms (see fuse_norms): from layer 1 on, the attention
+      // norm is the qkv GEMM's prologue on the residual the down projection
+      // left, and every post-attention norm the gate/up GEMM's
+      const bool fz_in = fuse && l > 0;
+      ffmi::FuseArgs fz_qkv, fz_o, fz_gu, fz_d;
+      if (fuse) {
+        fz_o.kind = fz_d.kind = 1;
+        fz_o.res_in = fz_d.res_in = res;
+        fz_o.ss_out = ss_o, fz_d.ss_out = ss_d;
+        fz_qkv.kind = fz_gu.kind = 2;
+        fz_qkv.ss_in = ss_d, fz_gu.ss_in = ss_o;
+        fz_qkv.nss = fz_gu.nss = H / 16;
+        fz_qkv.wnorm = L.in_norm, fz_gu.wnorm = L.post_norm;
+        fz_qkv.eps = fz_gu.eps = eps;
+      }
+      if (!fz_in) {
+        pr = prof_begin(on);
+        // layer 0: the embedding lookup gathers straight into the first norm
+        // (embedding_kernels.cu:233-244; res = the looked-up rows)
+        FFMI_HIP(ffmi::launch_rmsnorm(l == 0 ? embed : res, l == 0 ? nullptr : proj, L.in_norm, res,
+                                      h, T, H, eps, stream, packed,
+                                      l == 0 ? ffmi::Partials() : down_part,
+                                      l == 0 ? (blob_fetch ? batch->host : batch->dev) : nullptr,
+                                      l == 0 && blob_fetch ? batch->dev : nullptr, blob_bytes));
+        // the staging is free for the next step once the fetch has read it
+        if (l == 0 && blob_fetch && record_upload) FFMI_HIP(hipEventRecord(batch->uploaded, stream));
+        prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
+        mk();
+      }
       if (dbg) {
         // residual stream after layer l-1 (layer 0: the embedding rows)
         TRY(dbg_copy(l == 0 ? FFMI_DBG_EMBED : FFMI_DBG_HIDDEN, l == 0 ? 0 : l - 1, res, T));
@@ -725,8 +755,9 @@ struct LlamaGPU : public ffmi_model {
       }
       pr = prof_begin(on);
       ffmi::Partials qkv_part;
-      FFMI_HIP(ffmi::launch_gemm(h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H, XP, stream,
-                                 &qkv_part));
+      FFMI_HIP(ffmi::launch_gemm(fz_in ? res : h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H,
+                                 fz_in ? wstream : XP, stream, &qkv_part, 0,
+                                 fz_in ? &fz_qkv : nullptr));
       prof_end(pr, GEMM_QKV, gemm_bytes(T, 3 * Hl, 3 * Hl, H), 2.0 * T * 3 * Hl * H);
       mk();
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_QKV, l, qkv, qkv_part, T));
@@ -737,7 +768,13 @@ struct LlamaGPU : public ffmi_model {
       mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_ATTN_OUT, l, att, T));
       ffmi::Partials o_part;
-      if (o.tp_size == 1 || solo) {
+      if (fuse) {  // o projection + residual add (+ sums of squares): res in place
+        pr = prof_begin(on);
+        FFMI_HIP(ffmi::launch_gemm(att, L.wo, res, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
+                                   nullptr, 0, &fz_o));
+        prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
+        mk();
+      } else if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
                                    H <= 8192 ? &o_part : nullptr));
@@ -750,19 +787,32 @@ struct LlamaGPU : public ffmi_model {
         mk();
       }
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_O_PROJ, l, proj, o_part, T));
-      pr = prof_begin(on);
-      FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
-                                    o_part));
-      prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
-      mk();
+      if (!fuse) {
+        pr = prof_begin(on);
+        FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
+                                      o_part));
+        prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+        mk();
+      }
       if (dbg) TRY(dbg_copy(FFMI_DBG_FFN_NORM, l, h, T));
       pr = prof_begin(on);
       const int YP = packed ? FFMI_Y_PACKED : 0;
-      TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
+      if (fuse)
+        FFMI_HIP(ffmi::launch_gemm(res, L.wgu, mlp, (float *)ws, ws_bytes, T, Fl, H,
+                                   FFMI_EPI_SILU_MUL | YP | wstream, stream, nullptr, 0, &fz_gu));
+      else
+        TRY(ffmi_linear_ws(h, L.wgu, mlp, T, Fl, H, FFMI_EPI_SILU_MUL | XP | YP, ws, ws_bytes, s));
       prof_end(pr, GEMM_GATE_UP, gemm_bytes(T, 2 * Fl, Fl, H), 2.0 * T * 2 * Fl * H);
       mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_MLP_ACT, l, mlp, T));
-      if (o.tp_size == 1 || solo) {
+      if (fuse) {  // down projection + residual add (+ sums of squares)
+        pr = prof_begin(on);
+        FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, res, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
+                                   nullptr, 0, &fz_d));
+        prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
+        mk();
+        mk();
+      } else if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
                                    H <= 8192 ? &down_part : nullptr));
@@ -779,8 +829,11 @@ struct LlamaGPU : public ffmi_model {
     }
     const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
     pr = prof_begin(ptail);
-    FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
-                                  down_part));
+    if (fuse)  // res already holds the last residual add
+      FFMI_HIP(ffmi::launch_rmsnorm(res, nullptr, final_norm, nullptr, h, T, H, eps, stream, packed));
+    else
+      FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
+                                    down_part));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
     if (dbg) {
       TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers - 1, res, T));

@@ -314,3 +314,24 @@ def test_blob_fetch_same_tokens(monkeypatch, graphs):
         spec, _ = run_spec(ps, 60, SSM_CFG, 5)
         out.append(([r.output_tokens for r in inc], [r.output_tokens for r in spec]))
     assert out[0] == out[1]
+
+
+def test_fused_residual_norm_equals_norm_kernels(monkeypatch):
+    """The residual RMSNorms folded into the skinny GEMMs around them (o/down
+    add the residual and leave per-tile sums of squares; qkv and gate/up
+    normalise the residual they read -- the default at T <= 32) against the
+    separate norm kernels (FFMI_FUSE_NORM=0): identical tokens, or a first
+    divergence that is an oracle-checked fp16 tie (the rms sums its squares in
+    another order, and the 68M-like SSM's o/down run unsplit)."""
+    ps = prompts(4, 1000, 5, 40, 16)
+    out = []
+    for mode in ("2", "0"):  # forced at these widths (auto fuses only H >= 2048)
+        monkeypatch.setenv("FFMI_FUSE_NORM", mode)
+        inc, _ = run_incr(ps, 64)
+        spec, _ = run_spec(ps, 64, SSM_CFG, 5)
+        out.append(([r.output_tokens for r in inc], [r.output_tokens for r in spec]))
+    for kind in (0, 1):
+        for a, b, p in zip(out[0][kind], out[1][kind], ps):
+            if a != b:
+                check_tokens_vs_oracle(LLM_CFG, 11, a, len(p) + 1)
+                check_tokens_vs_oracle(LLM_CFG, 11, b, len(p) + 1)
