@@ -332,8 +332,9 @@ extern "C" ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *
 
 namespace ffmi {
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
-                         void *out, ffmi_stream stream, int parity) {
+                         void *out, ffmi_stream stream, int parity, OprojArgs *opa) {
   FFMI_CHECK(h && b && (qkv || qkvp.S > 0) && out, FFMI_ERR_INVALID);
+  if (opa) opa->done = false;
   FFMI_CHECK(b->num_tokens <= h->cfg.max_tokens, FFMI_ERR_INVALID);
   const bool tree = h->cfg.mode == FFMI_ATTN_TREE;
   const hipStream_t s = (hipStream_t)stream;
@@ -365,11 +366,16 @@ ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
                                     stage_rd, h->rope, heads, d, h->slots, h->slots, s));
     C = 0;
   }
+  // the output projection rides along where its launch allows it (fused,
+  // one query tile, d = 64, N <= 1024 columns); otherwise the caller runs it
+  const bool oproj = opa && opa->wo && opa->slab && fused && d == 64 && b->max_q <= 16 &&
+                     opa->N % 16 == 0 && opa->N <= 1024 && b->num_tokens <= opa->max_T;
   FFMI_HIP(ffmi::launch_attention(b->dev, b->num_work, b->max_q, h->qbuf, h->kc, h->vc,
                                   (uint16_t *)out, heads, d, h->slots, h->cfg.qk_scale, s,
                                   h->cfg.out_layout == 1, fused, b->num_tokens, C,
                                   (const uint16_t *)qkv, qkvp, stage_wr, stage_rd, h->rope,
-                                  h->slots));
+                                  h->slots, oproj ? opa : nullptr));
+  if (oproj) opa->done = true;
   return FFMI_OK;
 }
 }  // namespace ffmi

@@ -204,11 +204,25 @@ hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_
 hipError_t launch_commit(const char *blob, int C, const uint16_t *stage,
                          uint16_t *kc, uint16_t *vc, int heads, int d, int slots,
                          hipStream_t s);
+// Output projection folded into the fused attention (small models, where one
+// head's K-slice of Wo is a few tens of KB: the 68M SSM's is 96 KB).  Each
+// (work item, head) workgroup multiplies its rounded fp16 output rows [q][d]
+// by Wo[:, head*d .. head*d + d) and stores the fp32 product as slab `head`
+// of [heads][T][N]; the residual norm sums the heads in order and rounds once
+// (Partials), as it combines a split-K GEMM's slabs -- no o_proj launch.
+struct OprojArgs {
+  const uint16_t *wo = nullptr;  // packed [N][heads * d] (weights.hip)
+  float *slab = nullptr;         // [heads][T][N] fp32
+  int N = 0, max_T = 0;          // output width; rows the slab buffer holds
+  size_t wts = 0, wks = 0;       // packed-block strides (w_tile_stride / w_k_stride)
+  bool done = false;             // out: the launch projected (else run the o GEMM)
+};
 hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, uint16_t *kc,
                             uint16_t *vc, uint16_t *out, int heads, int d, int slots, float scale,
                             hipStream_t s, bool out_packed, bool fused, int T, int C,
                             const uint16_t *qkv, Partials qkvp, uint16_t *stage_wr,
-                            const uint16_t *stage_rd, const float *rope, int max_rope_pos);
+                            const uint16_t *stage_rd, const float *rope, int max_rope_pos,
+                            const OprojArgs *opa = nullptr);
 
 uint64_t weight_key(const char *name, uint64_t seed);
 
@@ -257,5 +271,6 @@ ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int row
 // FFMI_OK, or the transport's timeout error after a synchronised step
 ffmi_status comm_status(ffmi_comm *c);
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,
-                         void *out, ffmi_stream stream, int parity = -1);
+                         void *out, ffmi_stream stream, int parity = -1,
+                         OprojArgs *opa = nullptr);
 }  // namespace ffmi

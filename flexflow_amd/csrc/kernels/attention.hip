@@ -378,11 +378,19 @@ struct KvUpdateArgs {
 // own request's TREE commits and the KV update of its own tokens for its
 // head (kv_update_kernel's work), makes them visible to the workgroup, then
 // attends -- one launch per step instead of two.
-template <int D, int QT, int NW, bool FUSED, bool ST = false, int PSRC = -1>
+//
+// OP (FUSED, QT == 1; OprojArgs in ffmi_internal.h): the workgroup also
+// multiplies its rounded output rows by its head's K-slice of Wo (MFMA with
+// the packed weight block as the A operand and the output rows, from LDS, as
+// B -- the S^T = K.Q^T arrangement) and stores the fp32 product as slab
+// `head`.  The slice is loaded after the key loop, so the merge hides its
+// latency; wave w owns column tiles w, w + NW, ... (N <= 16 * 8 * NW).
+template <int D, int QT, int NW, bool FUSED, bool ST = false, int PSRC = -1, bool OP = false>
 __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     const char *__restrict__ blob, uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
     uint16_t *__restrict__ vc, uint16_t *__restrict__ out, int heads, int slots, float scale,
-    int out_packed, KvUpdateArgs kv) {
+    int out_packed, KvUpdateArgs kv, OprojArgs opa) {
+  static_assert(!OP || (FUSED && QT == 1), "output projection: fused, one query tile");
   constexpr int KS = D / 32;  // k-steps of the QK^T product
   constexpr int DT = D / 16;  // d-tiles of the PV product
   constexpr int NQ = 16 * QT;
@@ -697,6 +705,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   }
 
   stamp(3);
+  // OP: this head's K-slice of Wo (k-steps h*KS .. h*KS + KS - 1) for the
+  // wave's column tiles, in flight through the V^T stores and the merge
+  constexpr int OT = OP ? 8 : 1;
+  h8 wo_f[OT][KS];
+  const int o_tiles = OP ? opa.N >> 4 : 0;
+  if constexpr (OP) {
+#pragma unroll
+    for (int j = 0; j < OT; ++j) {
+      const int t = wave + j * NW;
+      if (t < o_tiles) {
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          wo_f[j][ks] = *reinterpret_cast<const h8 *>(opa.wo + (size_t)t * opa.wts +
+                                                      (size_t)(h * KS + ks) * opa.wks + lane * 8);
+      }
+    }
+  }
   if (FUSED) {
     // V^T of this step's tokens to HBM from the tail, by each wave once its
     // key loop is done (not waited for)
@@ -760,6 +785,30 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       uint16_t *dst = out_packed ? out + act_packed_off(orow_m, h * D + t * 16 + 4 * g, Hl)
                                  : orow + t * 16 + 4 * g;
       *reinterpret_cast<uint2 *>(dst) = pk;
+      // OP: the rounded row also to LDS (the queries' tile is free by now)
+      if (OP) *reinterpret_cast<uint2 *>(&sQ[q][t * 16 + 4 * g]) = pk;
+    }
+  }
+  if constexpr (OP) {
+    // slab[head][token][n] = sum_d out[token][head*d + d] * Wo[n][head*d + d]:
+    // lane (qi, g) ends with n = 16 t + 4 g + r of query qi.  Rows of queries
+    // past q_count hold stale LDS; their columns are computed, never stored.
+    __syncthreads();
+    h8 xb[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) xb[ks] = *reinterpret_cast<const h8 *>(&sQ[qi][32 * ks + 8 * g]);
+    const bool qv = qi < w.q_count;
+    float *srow = opa.slab + ((size_t)h * kv.T + w.q_start + qi) * opa.N + 4 * g;
+#pragma unroll
+    for (int j = 0; j < OT; ++j) {
+      const int t = wave + j * NW;
+      if (t < o_tiles) {
+        f4 c = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks)
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(wo_f[j][ks], xb[ks], c, 0, 0, 0);
+        if (qv) *reinterpret_cast<f4 *>(srow + t * 16) = c;
+      }
     }
   }
   if (ST && stp) {
@@ -778,13 +827,13 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
   do {                                                                                          \
     if (!FU)                                                                                    \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, false>), grid, dim3(512), 0, s, blob, qbuf, \
-                         kc, vc, out, heads, slots, scale, op, kv);                             \
+                         kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                             \
     else if (kv.part)                                                                           \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 1>), grid, dim3(512), 0, s,    \
-                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                 \
     else                                                                                        \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 0>), grid, dim3(512), 0, s,    \
-                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv);                 \
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                 \
   } while (0)
   // diagnostics build: FFMI_ATTN_STAMP=1 stamps the d = 128 (LLM) launches,
   // FFMI_ATTN_STAMP=64 the d = 64 (68M SSM) ones
@@ -794,10 +843,10 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
   do {                                                                                          \
     if (fused)                                                                                  \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, true>), grid, dim3(512), 0, s, blob,  \
-                         qbuf, kc, vc, out, heads, slots, scale, op, kv);                       \
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                       \
     else                                                                                        \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, false, true>), grid, dim3(512), 0, s, blob, \
-                         qbuf, kc, vc, out, heads, slots, scale, op, kv);                       \
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                       \
   } while (0)
     if (max_q > 16) FFMI_ATT_ST(2);
     else FFMI_ATT_ST(1);
@@ -874,7 +923,8 @@ hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, 
                             uint16_t *vc, uint16_t *out, int heads, int d, int slots, float scale,
                             hipStream_t s, bool out_packed, bool fused, int T, int C,
                             const uint16_t *qkv, Partials qkvp, uint16_t *stage_wr,
-                            const uint16_t *stage_rd, const float *rope, int max_rope_pos) {
+                            const uint16_t *stage_rd, const float *rope, int max_rope_pos,
+                            const OprojArgs *opa) {
   if (W <= 0) return hipSuccess;
   if (out_packed && (heads * d) % 32) return hipErrorInvalidValue;
   if (max_q > FFMI_ATTN_QTILE) return hipErrorInvalidValue;
@@ -882,6 +932,18 @@ hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, 
                         qkvp.S,   qkvp.NP,  stage_wr, stage_rd,
                         rope,     max_rope_pos, attn_stamp_buf(W * heads)};
   const int op = out_packed ? 1 : 0;
+  if (opa) {  // output projection folded in (the caller checked fused, d, max_q, N)
+    if (!fused || d != 64 || max_q > 16 || opa->N % 16 || opa->N > 16 * 8 * 8 || T > opa->max_T)
+      return hipErrorInvalidValue;
+    const dim3 grid(W, heads);
+    if (kv.part)
+      hipLaunchKernelGGL((attention_kernel<64, 1, 8, true, false, 1, true>), grid, dim3(512), 0, s,
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, *opa);
+    else
+      hipLaunchKernelGGL((attention_kernel<64, 1, 8, true, false, 0, true>), grid, dim3(512), 0, s,
+                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, *opa);
+    return hipGetLastError();
+  }
   if (d == 128)
     return launch_attention_d<128>(blob, W, max_q, qbuf, kc, vc, out, heads, slots, scale, s, op,
                                    fused, kv);

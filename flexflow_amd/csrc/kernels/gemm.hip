@@ -1084,7 +1084,8 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
 
 hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, hipStream_t s) {
   if (T <= 0 || p.S <= 0) return hipSuccess;
-  if (p.S > 8 || p.NP % 16 || N > p.NP) return hipErrorInvalidValue;
+  // (> 8: the per-head o-projection slabs of a small model, OprojArgs)
+  if (p.S > 16 || p.NP % 16 || N > p.NP) return hipErrorInvalidValue;
   const long total = (long)T * ((N + 3) / 4);
   const unsigned blocks = (unsigned)((total + 255) / 256);
 #define FFMI_PRED(MS)                                                                          \
@@ -1092,7 +1093,8 @@ hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, 
                      p.NP / 16, p.S, 0)
   if (p.S <= 2) FFMI_PRED(2);
   else if (p.S <= 4) FFMI_PRED(4);
-  else FFMI_PRED(8);
+  else if (p.S <= 8) FFMI_PRED(8);
+  else FFMI_PRED(16);
 #undef FFMI_PRED
   return hipGetLastError();
 }

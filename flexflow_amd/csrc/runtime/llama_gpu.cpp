@@ -79,6 +79,13 @@ struct LlamaGPU : public ffmi_model {
   // 1 auto (default), 2 every width (tests)
   int fuse_norms = getenv("FFMI_FUSE_NORM") ? atoi(getenv("FFMI_FUSE_NORM")) : 1;
   float *ss_o = nullptr, *ss_d = nullptr;
+  // output projection folded into the fused attention (ffmi::OprojArgs): a
+  // small model (d = 64, H <= 1024 -- the 68M SSM) at TP = 1 skips its o_proj
+  // launch; the attention leaves one fp32 slab per head [heads][T][H] for the
+  // residual norm.  FFMI_FUSE_AO=0 turns it off (A/B, tests)
+  bool fuse_ao = false;
+  float *oslab = nullptr;
+  int oslab_T = 0;
   int tp_chunks = 1;
   hipStream_t comm_stream = nullptr;
   uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
@@ -395,6 +402,12 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&ss_o, (size_t)2 * 32 * (H / 16)));
     ss_d = ss_o + (size_t)32 * (H / 16);
     TRY(alloc(&mlp, (size_t)Tm * Fl));
+    fuse_ao = P == 1 && d == 64 && H <= 1024 && H % 16 == 0 &&
+              !(getenv("FFMI_FUSE_AO") && atoi(getenv("FFMI_FUSE_AO")) == 0);
+    if (fuse_ao) {  // decode / beam steps (<= 64 rows); prefill blocks run the GEMM
+      oslab_T = std::min(Tm, 64);
+      TRY(alloc(&oslab, (size_t)heads_l * oslab_T * H));
+    }
     Vl = P > 1 && V % P == 0 && (V / P) % 16 == 0 ? V / P : V;
     if (const char *e = getenv("FFMI_VOCAB_SHARD"))  // A/B: 0 = replicated lm_head
       if (!atoi(e)) Vl = V;
@@ -762,13 +775,21 @@ struct LlamaGPU : public ffmi_model {
       mk();
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_QKV, l, qkv, qkv_part, T));
       pr = prof_begin(on);
+      ffmi::OprojArgs oa;
+      if (fuse_ao && !fuse) {
+        oa.wo = L.wo, oa.slab = oslab, oa.N = H, oa.max_T = oslab_T;
+        oa.wts = ffmi::w_tile_stride(Hl / 32), oa.wks = ffmi::w_k_stride(H / 16);
+      }
       TRY(ffmi::attn_forward(L.attn, batch, qkv, qkv_part, att, s,
-                             mode == FFMI_MODEL_TREE ? tree_parity : -1));
+                             mode == FFMI_MODEL_TREE ? tree_parity : -1,
+                             oa.wo ? &oa : nullptr));
       prof_end(pr, ATTENTION, on ? attn_bytes() : 0, 0);
       mk();
       if (dbg) TRY(dbg_copy(FFMI_DBG_ATTN_OUT, l, att, T));
       ffmi::Partials o_part;
-      if (fuse) {  // o projection + residual add (+ sums of squares): res in place
+      if (oa.done) {  // the attention projected: one slab per head
+        o_part.p = oslab, o_part.S = heads_l, o_part.NP = H;
+      } else if (fuse) {  // o projection + residual add (+ sums of squares): res in place
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_gemm(att, L.wo, res, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
                                    nullptr, 0, &fz_o));
