@@ -458,6 +458,27 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   h8 kf0[2][KS], va0[DT];
   const bool early = FUSED && wave < nchunks && wave < ctail;
 
+  // OP: this head's K-slice of Wo (k-steps h*KS .. h*KS + KS - 1) for the
+  // wave's column tiles, issued right behind the prologue's loads (and the
+  // first K/V chunk), so the KV update, key loop and merge hide its latency
+  constexpr int OT = OP ? 8 : 1;
+  h8 wo_f[OT][KS];
+  const int o_tiles = OP ? opa.N >> 4 : 0;
+  auto load_wo = [&]() {
+    if constexpr (OP) {
+#pragma unroll
+      for (int j = 0; j < OT; ++j) {
+        const int t = wave + j * NW;
+        if (t < o_tiles) {
+#pragma unroll
+          for (int ks = 0; ks < KS; ++ks)
+            wo_f[j][ks] = *reinterpret_cast<const h8 *>(opa.wo + (size_t)t * opa.wts +
+                                                        (size_t)(h * KS + ks) * opa.wks + lane * 8);
+        }
+      }
+    }
+  };
+
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
   __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
   __shared__ int4 sMrec[FUSED ? NQ : 1];
@@ -532,6 +553,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
           }
           // (issued last: the waits below for the loads above leave it in flight)
           if (early) load_chunk(wave, kf0, va0);
+          load_wo();
         },
         [&] {  // loads are back: the old tail to LDS, then the commits
           stamp(10);
@@ -705,23 +727,6 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   }
 
   stamp(3);
-  // OP: this head's K-slice of Wo (k-steps h*KS .. h*KS + KS - 1) for the
-  // wave's column tiles, in flight through the V^T stores and the merge
-  constexpr int OT = OP ? 8 : 1;
-  h8 wo_f[OT][KS];
-  const int o_tiles = OP ? opa.N >> 4 : 0;
-  if constexpr (OP) {
-#pragma unroll
-    for (int j = 0; j < OT; ++j) {
-      const int t = wave + j * NW;
-      if (t < o_tiles) {
-#pragma unroll
-        for (int ks = 0; ks < KS; ++ks)
-          wo_f[j][ks] = *reinterpret_cast<const h8 *>(opa.wo + (size_t)t * opa.wts +
-                                                      (size_t)(h * KS + ks) * opa.wks + lane * 8);
-      }
-    }
-  }
   if (FUSED) {
     // V^T of this step's tokens to HBM from the tail, by each wave once its
     // key loop is done (not waited for)
