@@ -385,15 +385,28 @@ struct KvUpdateArgs {
 // B -- the S^T = K.Q^T arrangement) and stores the fp32 product as slab
 // `head`.  The slice is loaded after the key loop, so the merge hides its
 // latency; wave w owns column tiles w, w + NW, ... (N <= 16 * 8 * NW).
-template <int D, int QT, int NW, bool FUSED, bool ST = false, int PSRC = -1, bool OP = false>
+//
+// QS == 2 (FUSED, QT == 1; grids with CUs to spare: TP >= 2 verify steps,
+// <= 128 (request, head) pairs): the item's queries are split over two
+// workgroups (blockIdx.z = which 16), each running the whole item's commits
+// and KV update -- the same values to the same addresses, and every K/V it
+// reads from memory is below the tail, which neither writes -- and attending
+// its own 16: the key loop and merge work per workgroup halve.  Per query the
+// arithmetic is the QT == 2 kernel's (MFMA columns are independent), so the
+// output is bit-identical.
+template <int D, int QT, int NW, bool FUSED, bool ST = false, int PSRC = -1, bool OP = false,
+          int QS = 1>
 __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     const char *__restrict__ blob, uint16_t *__restrict__ qbuf, uint16_t *__restrict__ kc,
     uint16_t *__restrict__ vc, uint16_t *__restrict__ out, int heads, int slots, float scale,
     int out_packed, KvUpdateArgs kv, OprojArgs opa) {
-  static_assert(!OP || (FUSED && QT == 1), "output projection: fused, one query tile");
+  static_assert(!OP || (FUSED && QT == 1 && QS == 1), "output projection: fused, one query tile");
+  static_assert(QS == 1 || (FUSED && QT == 1 && QS == 2), "query split: fused, 2 x 16 queries");
   constexpr int KS = D / 32;  // k-steps of the QK^T product
   constexpr int DT = D / 16;  // d-tiles of the PV product
-  constexpr int NQ = 16 * QT;
+  constexpr int NQ = 16 * QT;   // queries this workgroup attends
+  constexpr int NQK = NQ * QS;  // tokens of the item (commits, KV update)
+  const int qbase = QS > 1 ? (int)blockIdx.z * NQ : 0;
   constexpr int TS = kTailSlots;
   __shared__ float sm_m[NW][NQ];
   __shared__ float sm_l[NW][NQ];
@@ -480,10 +493,10 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   };
 
   // FUSED: this item's rotated queries stay in LDS (rows padded by 16 B)
-  __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQ : 1][D + 8];
-  __shared__ int4 sMrec[FUSED ? NQ : 1];
-  __shared__ int sSlotV[FUSED ? NQ : 1];
-  __shared__ uint64_t sMvis[FUSED ? NQ : 1];
+  __shared__ __attribute__((aligned(16))) uint16_t sQ[FUSED ? NQK : 1][D + 8];
+  __shared__ int4 sMrec[FUSED ? NQK : 1];
+  __shared__ int sSlotV[FUSED ? NQK : 1];
+  __shared__ uint64_t sMvis[FUSED ? NQK : 1];
   if (FUSED) {
     int *sSlot = sSlotV;
     const WorkDev *wdp = &bv.work[blockIdx.x];
@@ -521,7 +534,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
       csrc[i] = (int)(int16_t)((j & 1) ? (wd >> 16) : (wd & 0xffffu));
     }
     uint4 cmv[CP];
-    kv_update_item<D, NQ, NT, PSRC>(
+    kv_update_item<D, NQK, NT, PSRC>(
         bv, wdp, h, heads, slots, kv.T, kv.qkv, kv.part, kv.pS, kv.pNP, kv.rope, kv.max_rope_pos,
         qbuf, kc, kv.stage_wr, nullptr, sSlot, sQ, sKt, sVt, tail0,
         [&] {  // after the KV update's own loads: commits, tail, first chunk
@@ -546,7 +559,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
             if (dd < D && s8 < told)
               tv[i] = *reinterpret_cast<const uint4 *>(vbase + (size_t)dd * slots + tail0 + s8);
           }
-          if ((int)threadIdx.x < NQ) {
+          if ((int)threadIdx.x < NQK) {
             const ffmi_token_info *ti = &bv.tokens[w.q_start + min((int)threadIdx.x, max(w.q_count - 1, 0))];
             mrec = make_int4(ti->prefix_len, ti->tree_base, ti->tree_len, 0);
             mvis = ti->tree_vis;
@@ -557,7 +570,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
         },
         [&] {  // loads are back: the old tail to LDS, then the commits
           stamp(10);
-          if ((int)threadIdx.x < NQ) sMrec[threadIdx.x] = mrec, sMvis[threadIdx.x] = mvis;
+          if ((int)threadIdx.x < NQK) sMrec[threadIdx.x] = mrec, sMvis[threadIdx.x] = mvis;
 #pragma unroll
           for (int i = 0; i < TK; ++i) {
             const int e = threadIdx.x + i * NT, row = e / D8;
@@ -621,7 +634,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   h8 qf[QT][KS];
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    const int q = qt * 16 + qi;
+    const int q = qbase + qt * 16 + qi;
     qvalid[qt] = q < w.q_count;
     if (FUSED) {
       const int4 mr = sMrec[qvalid[qt] ? q : 0];
@@ -731,8 +744,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     // V^T of this step's tokens to HBM from the tail, by each wave once its
     // key loop is done (not waited for)
     uint16_t *vt = vc + ((size_t)w.req * heads + h) * D * slots;
-    for (int e = threadIdx.x; e < D * NQ; e += blockDim.x) {
-      const int dd = e / NQ, tt = e % NQ;
+    for (int e = threadIdx.x; e < D * NQK; e += blockDim.x) {
+      const int dd = e / NQK, tt = e % NQK;
       if (tt >= w.q_count) continue;
       const int sl = sSlotV[tt];
       if (sl >= 0) vt[(size_t)dd * slots + sl] = sVt[dd][sl - tail0];
@@ -760,16 +773,16 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   // merge: wave w finalizes d-tiles t = w, w+NW, ... of every query tile
 #pragma unroll
   for (int qt = 0; qt < QT; ++qt) {
-    const int q = qt * 16 + qi;
+    const int ql = qt * 16 + qi, q = qbase + ql;  // in the workgroup / in the item
     float M = NEG;
 #pragma unroll
-    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, sm_m[ww][q]);
+    for (int ww = 0; ww < NW; ++ww) M = fmaxf(M, sm_m[ww][ql]);
     float f[NW], L = 0.f;
 #pragma unroll
     for (int ww = 0; ww < NW; ++ww) {
-      const float mw = sm_m[ww][q];
+      const float mw = sm_m[ww][ql];
       f[ww] = (mw == NEG) ? 0.f : __expf(mw - M);
-      L += f[ww] * sm_l[ww][q];
+      L += f[ww] * sm_l[ww][ql];
     }
     const float inv = 1.0f / (L + 1e-6f);
     if (!qvalid[qt]) continue;
@@ -822,6 +835,23 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
   }
 }
 
+// Query split (attention_kernel QS == 2) of a fused launch with more than 16
+// queries per item: when the (item, head) grid leaves half the CUs idle
+// (TP >= 2 verify steps).  FFMI_ATTN_QSPLIT: 0 off, 1 auto (default), 2
+// always (tests; read at every launch, so a test can switch it).
+static bool attn_qsplit(int wgs) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = 256;
+  }
+  const char *e = getenv("FFMI_ATTN_QSPLIT");
+  const int mode = e ? atoi(e) : 1;
+  return mode == 2 || (mode == 1 && 2 * wgs <= cus);
+}
+
 template <int D>
 static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_t *qbuf,
                                      uint16_t *kc, uint16_t *vc, uint16_t *out, int heads,
@@ -856,6 +886,16 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
     if (max_q > 16) FFMI_ATT_ST(2);
     else FFMI_ATT_ST(1);
 #undef FFMI_ATT_ST
+    return hipGetLastError();
+  }
+  if (max_q > 16 && fused && attn_qsplit(W * heads)) {
+    const dim3 grid2(W, heads, 2);
+    if (kv.part)
+      hipLaunchKernelGGL((attention_kernel<D, 1, 8, true, false, 1, false, 2>), grid2, dim3(512), 0,
+                         s, blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
+    else
+      hipLaunchKernelGGL((attention_kernel<D, 1, 8, true, false, 0, false, 2>), grid2, dim3(512), 0,
+                         s, blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
     return hipGetLastError();
   }
   if (max_q <= 16) {

@@ -526,8 +526,10 @@ def test_attention_tree_verify_and_commit(d):
 @pytest.mark.parametrize("d", [64, 128])
 def test_attention_tree_fused_equals_two_launch_path(d, monkeypatch):
     """Verify steps (21-token trees for two requests, commits of the previous
-    step) through the one-launch path and the KV-update + attention path:
-    outputs, K cache and V^T cache bit-identical."""
+    step) through the one-launch path -- with the item's queries split over
+    two workgroups (FFMI_ATTN_QSPLIT=2, the TP >= 2 form) and unsplit -- and
+    the KV-update + attention path: outputs, K cache and V^T cache
+    bit-identical."""
     def scenario():
         rng = np.random.default_rng(300 + d)
         c = AttnCase(F.ATTN_TREE, d=d)
@@ -553,11 +555,15 @@ def test_attention_tree_fused_equals_two_launch_path(d, monkeypatch):
         hip().hipMemcpy(kc.ctypes.data, k, n * 2, 2)
         hip().hipMemcpy(vc.ctypes.data, v, n * 2, 2)
         return o1, o2, o3, kc, vc
+    monkeypatch.setenv("FFMI_ATTN_QSPLIT", "2")
+    qsplit = scenario()
+    monkeypatch.setenv("FFMI_ATTN_QSPLIT", "0")
     fused = scenario()
     monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
     split = scenario()
-    for a, b in zip(fused, split):
+    for a, b, c in zip(qsplit, fused, split):
         assert np.array_equal(np.asarray(a).view(np.uint16), np.asarray(b).view(np.uint16))
+        assert np.array_equal(np.asarray(b).view(np.uint16), np.asarray(c).view(np.uint16))
 
 
 def test_attention_spec_beam_layers():
