@@ -1,4 +1,8 @@
 // capi.cpp -- C ABI of the serving runtime (models + RequestManager).
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
 #include <vector>
 
 #include "request_manager.h"
@@ -44,7 +48,17 @@ extern "C" ffmi_status ffmi_set_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FFMI_ERR_NO_DEVICE;
   if (device < 0 || device >= n) return FFMI_ERR_INVALID;
-  return hipSetDevice(device) == hipSuccess ? FFMI_OK : FFMI_ERR_HIP;
+  if (hipSetDevice(device) != hipSuccess) return FFMI_ERR_HIP;
+  // FFMI_SYNC=spin|yield|block: how a host thread waits in hipStreamSynchronize
+  // (A/B of the per-step host round trip; left to HIP's default otherwise).
+  // Only before the device's context is live; later calls report an error.
+  if (const char *e = getenv("FFMI_SYNC")) {
+    const unsigned f = !strcmp(e, "spin") ? hipDeviceScheduleSpin
+                       : !strcmp(e, "yield") ? hipDeviceScheduleYield
+                       : hipDeviceScheduleBlockingSync;
+    if (hipSetDeviceFlags(f) != hipSuccess) fprintf(stderr, "ffmi: FFMI_SYNC=%s not applied\n", e);
+  }
+  return FFMI_OK;
 }
 
 extern "C" ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out) {
