@@ -55,8 +55,9 @@ extern "C" ffmi_status ffmi_set_device(int device) {
   if (const char *e = getenv("FFMI_SYNC")) {
     const unsigned f = !strcmp(e, "spin") ? hipDeviceScheduleSpin
                        : !strcmp(e, "yield") ? hipDeviceScheduleYield
-                       : hipDeviceScheduleBlockingSync;
-    if (hipSetDeviceFlags(f) != hipSuccess) fprintf(stderr, "ffmi: FFMI_SYNC=%s not applied\n", e);
+                       : !strcmp(e, "block") ? hipDeviceScheduleBlockingSync : 0u;
+    if (!f || hipSetDeviceFlags(f) != hipSuccess)
+      fprintf(stderr, "ffmi: FFMI_SYNC=%s not applied (spin, yield or block, before first use)\n", e);
   }
   return FFMI_OK;
 }
