@@ -312,6 +312,23 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   return FFMI_OK;
 }
 
+namespace ffmi {
+// FFMI_FAULT_ROPE_POS (tests only): positions >= from_pos rotate as
+// position + 1; from_pos < 0 restores the true table
+ffmi_status attn_rope_fault(ffmi_attn *h, int from_pos) {
+  FFMI_CHECK(h, FFMI_ERR_INVALID);
+  std::vector<float> tab;
+  rope_table(tab, h->slots + 1, h->cfg.head_dim, &h->cfg);
+  const size_t row = (size_t)h->cfg.head_dim;
+  if (from_pos >= 0)
+    for (int p = h->slots - 1; p >= std::max(from_pos, 0); --p)
+      memcpy(&tab[p * row], &tab[(p + 1) * row], row * sizeof(float));
+  FFMI_HIP(hipMemcpy(h->rope, tab.data(), (size_t)h->slots * row * sizeof(float),
+                     hipMemcpyHostToDevice));
+  return FFMI_OK;
+}
+}  // namespace ffmi
+
 extern "C" void ffmi_attn_destroy(ffmi_attn *h) {
   if (!h) return;
   (void)hipFree(h->kc);
@@ -537,6 +554,46 @@ extern "C" ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, in
   FFMI_CHECK(logits && ids && V > 0 && k >= 1 && k <= 4 && k <= V, FFMI_ERR_INVALID);
   FFMI_HIP(ffmi::launch_argmax((const uint16_t *)logits, T, V, k, ids, probs,
                                (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+// Test hooks of the residual RMSNorm folded into the decode GEMMs (the pair
+// llama_gpu.cpp runs at T <= 32): the producer adds its rounded output to
+// the residual in place and leaves per-(row, 16-column tile) sums of
+// squares; the consumer normalises the residual from those sums in its
+// prologue.  Row-major fp16 throughout.
+extern "C" ffmi_status ffmi_debug_fused_residual_linear(const void *X, const void *W_packed,
+                                                        void *residual, float *ss_out, int T,
+                                                        int out_dim, int in_dim,
+                                                        ffmi_stream stream) {
+  FFMI_CHECK(X && W_packed && residual && ss_out && T > 0 && T <= 32, FFMI_ERR_INVALID);
+  ffmi::FuseArgs fz;
+  fz.kind = 1;
+  fz.res_in = (const uint16_t *)residual;
+  fz.ss_out = ss_out;
+  FFMI_HIP(ffmi::launch_gemm((const uint16_t *)X, (const uint16_t *)W_packed, (uint16_t *)residual,
+                             nullptr, 0, T, out_dim, in_dim, FFMI_EPI_NONE, (hipStream_t)stream,
+                             nullptr, 0, &fz));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_debug_fused_norm_linear(const void *residual, const float *ss_in,
+                                                    const void *norm_w, float eps,
+                                                    const void *W_packed, void *Y, int T,
+                                                    int out_dim, int in_dim, int epilogue,
+                                                    ffmi_stream stream) {
+  FFMI_CHECK(residual && ss_in && norm_w && W_packed && Y && T > 0 && T <= 32 &&
+                 (epilogue == FFMI_EPI_NONE || epilogue == FFMI_EPI_SILU_MUL),
+             FFMI_ERR_INVALID);
+  ffmi::FuseArgs fz;
+  fz.kind = 2;
+  fz.ss_in = ss_in;
+  fz.nss = in_dim / 16;
+  fz.wnorm = (const uint16_t *)norm_w;
+  fz.eps = eps;
+  FFMI_HIP(ffmi::launch_gemm((const uint16_t *)residual, (const uint16_t *)W_packed, (uint16_t *)Y,
+                             nullptr, 0, T, out_dim, in_dim, epilogue, (hipStream_t)stream,
+                             nullptr, 0, &fz));
   return FFMI_OK;
 }
 

@@ -126,8 +126,10 @@ __device__ __forceinline__ float partials_value(const float *p, int S, int NP, i
 }
 
 // ---- kernel launchers (defined in kernels/*.hip) ----
-hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
-                              hipStream_t s);
+hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind, hipStream_t s,
+                              int cols = 0, uint64_t pa = 1, uint64_t pb = 0, float scale = 1.0f);
+float weight_amp(int kind);
+ffmi_status attn_rope_fault(ffmi_attn *h, int from_pos);
 // Packed weights (weights.hip): 1 KiB block (tile t, k-step kt) at
 // t * w_tile_stride(KT) + kt * w_k_stride(P) halves, P = tiles per k-row of
 // the allocation.  K-major unless FFMI_W_TILE_MAJOR=1 (A/B runs).

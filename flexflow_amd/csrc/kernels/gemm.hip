@@ -71,11 +71,15 @@ __device__ __forceinline__ float lane_f(float v, int l) {
 }
 
 // FZ (FuseArgs, ffmi_internal.h): 1 = residual-add producer epilogue (EPI 0,
-// unsplit), 2 = RMSNorm consumer prologue on row-major X.
+// unsplit), 2 = RMSNorm consumer prologue on row-major X.  Y is restrict-
+// qualified except in the producer, where it aliases fz.res_in (the residual
+// is updated in place).
+template <int FZ>
+using SkinnyY = std::conditional_t<FZ == 1, uint16_t *, uint16_t *__restrict__>;
 template <int MT, int NT, int KW, int U, int EPI, bool PIPE = false, bool NTL = false, int FZ = 0>
 __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
-    uint16_t *Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
+    SkinnyY<FZ> Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
     int NTILES, int xp, int yp, size_t wts, size_t wks, FuseArgs fz) {
   extern __shared__ __attribute__((aligned(16))) float red[];
   const int lane = threadIdx.x & 63;
@@ -120,6 +124,17 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         pv[rr][c] = fz.ss_in[(size_t)m * fz.nss + min(lane + 64 * c, fz.nss - 1)];
     }
   }
+  // rms_finish contains the workgroup's only __syncthreads before the
+  // cross-wave reduction.  It is called at several points (after the first
+  // batch of loads of the pipelined loop, the batched loop or the tail, and
+  // unconditionally after the k-loop) and runs once per wave (rdone): a wave
+  // whose k-range is empty, or shorter than a batch, reaches it at the
+  // post-loop call, so waves may arrive at s_barrier from different
+  // program points.  That is well defined on CDNA (s_barrier counts waves,
+  // not PCs); the builtin is convergent, so the compiler neither duplicates
+  // nor moves it across the rdone branch.  Pinned by
+  // test_gpu_kernels.py::test_fused_norm_consumer_empty_wave_ranges (KW 4 /
+  // 8 with waves that own no k-step, T 1..32).
   auto rms_finish = [&]() {
     if constexpr (FZ == 2) {
       if (rdone) return;

@@ -26,12 +26,17 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-__global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, int kind) {
-  const float center = kind == 1 ? 1.0f : 0.0f;
-  const float amp = kind == 1 ? 0.1f : 0.034641016f;
+// value i: element src(i) of the stream, src = i, or for a row-permuted
+// [rows][cols] tensor (cols > 0) element (perm(r), c), perm(r) = (r * pa + pb)
+// mod rows (the token-chain init's tied lm_head, oracle.h orc_gen_weight_rows)
+__global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, float center, float amp,
+                                   int cols, uint64_t pa, uint64_t pb) {
+  const uint64_t rows = cols > 0 ? n / cols : 1;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
-    uint64_t x = splitmix64(key + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    uint64_t src = i;
+    if (cols > 0) src = ((i / cols) * pa + pb) % rows * cols + i % cols;
+    uint64_t x = splitmix64(key + (src + 1) * 0x9E3779B97F4A7C15ull);
     float u = (float)(x >> 40) * (1.0f / 16777216.0f);
     float t = __fsub_rn(__fmul_rn(2.0f, u), 1.0f);
     float w = __fadd_rn(center, __fmul_rn(t, amp));
@@ -39,13 +44,21 @@ __global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, int ki
   }
 }
 
-hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind,
-                              hipStream_t s) {
+// amplitude of a weight kind (oracle.h orc_weight_amp: the same host float
+// operations, so both generators hold identical values)
+float weight_amp(int kind) {
+  if (kind == 1) return 0.1f;
+  if (kind & FFMI_WKIND_DEPTH) return 0.034641016f / sqrtf((float)(2 * (kind & 0xffff)));
+  return 0.034641016f;
+}
+
+hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind, hipStream_t s,
+                              int cols, uint64_t pa, uint64_t pb, float scale) {
   if (n == 0) return hipSuccess;
   size_t blocks = (n + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(fill_weight_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, n,
-                     key, kind);
+  hipLaunchKernelGGL(fill_weight_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, n, key,
+                     kind == 1 ? 1.0f : 0.0f, weight_amp(kind) * scale, cols, pa, pb);
   return hipGetLastError();
 }
 

@@ -44,6 +44,11 @@ extern "C" long ffmi_model_debug_width(ffmi_model *m, int which) {
   return m->debug_width(which);
 }
 
+extern "C" ffmi_status ffmi_model_debug_fault(ffmi_model *m, int kind, int layer, int arg) {
+  if (!m) return FFMI_ERR_INVALID;
+  return m->debug_fault(kind, layer, arg);
+}
+
 extern "C" ffmi_status ffmi_set_device(int device) {
   int n = 0;
   if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return FFMI_ERR_NO_DEVICE;

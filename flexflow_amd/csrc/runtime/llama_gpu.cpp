@@ -292,6 +292,25 @@ struct LlamaGPU : public ffmi_model {
     return T;
   }
 
+  ffmi_status debug_fault(int kind, int layer, int arg) override {
+    if (kind == FFMI_FAULT_NONE) {
+      for (auto &L : layers) {
+        ffmi_status st = ffmi::attn_rope_fault(L.attn, -1);
+        if (st != FFMI_OK) return st;
+      }
+      return FFMI_OK;
+    }
+    FFMI_CHECK(kind == FFMI_FAULT_ROPE_POS && layer >= -1 && layer < c.num_layers,
+               FFMI_ERR_INVALID);
+    if (stream) FFMI_HIP(hipStreamSynchronize(stream));
+    for (int l = 0; l < c.num_layers; ++l)
+      if (layer < 0 || l == layer) {
+        ffmi_status st = ffmi::attn_rope_fault(layers[l].attn, arg);
+        if (st != FFMI_OK) return st;
+      }
+    return FFMI_OK;
+  }
+
   ~LlamaGPU() override {
     if (stream) (void)hipStreamSynchronize(stream);
     clear_graphs();
@@ -471,16 +490,29 @@ struct LlamaGPU : public ffmi_model {
     uint16_t *tmp = nullptr;
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
     TRY(alloc(&tmp, tmp_elems));
-    auto fill = [&](uint16_t *dst, size_t n, const std::string &name, int kind) {
+    // synthetic inits (ffmi_model_opts.weight_init; oracle orc_model_create_ex):
+    // 1 scales o/down by 1/sqrt(2L); 2 (token chain) scales the embeddings by
+    // 128 and makes lm_head the permuted unscaled embedding rows
+    FFMI_CHECK(o.weight_init >= 0 && o.weight_init <= 2, FFMI_ERR_INVALID);
+    const int kres = o.weight_init == 1 ? (FFMI_WKIND_DEPTH | c.num_layers) : 0;
+    auto fill = [&](uint16_t *dst, size_t n, const std::string &name, int kind, int cols = 0,
+                    uint64_t pa = 1, float scale = 1.0f) -> ffmi_status {
       if (!weights_folder.empty()) return load_tensor(dst, n, name);
-      return ffmi_fill_weight(dst, n, name.c_str(), o.weight_seed, kind, (ffmi_stream)stream);
+      FFMI_CHECK(dst, FFMI_ERR_INVALID);
+      FFMI_HIP(ffmi::launch_fill_weight(dst, n, ffmi::weight_key(name.c_str(), o.weight_seed), kind,
+                                        stream, cols, pa, 17, scale));
+      return FFMI_OK;
     };
+    const bool chain = o.weight_init == 2 && weights_folder.empty();
     TRY(alloc(&embed, (size_t)V * H));
-    TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0));
+    TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0, 0, 1, chain ? 128.0f : 1.0f));
     TRY(alloc(&final_norm, H));
     TRY(fill(final_norm, H, "model.norm.weight", 1));
     TRY(alloc(&lm, ffmi_linear_packed_bytes(Vl, H) / 2));
-    TRY(fill(tmp, (size_t)V * H, "lm_head.weight", 0));
+    if (chain)
+      TRY(fill(tmp, (size_t)V * H, "model.embed_tokens.weight", 0, H, 7919));
+    else
+      TRY(fill(tmp, (size_t)V * H, "lm_head.weight", 0));
     // vocab shard s: rows [s*Vl, (s+1)*Vl) (the whole table when replicated)
     FFMI_HIP(launch_pack_weight(tmp, H, Vl == V ? 0 : o.tp_rank * Vl, 0, Vl, H, lm, 1, 0,
                                 (Vl + 15) / 16, stream));
@@ -507,7 +539,7 @@ struct LlamaGPU : public ffmi_model {
       }
       // o_proj: row-parallel -> columns [s*Hl, (s+1)*Hl)
       TRY(alloc(&L.wo, ffmi_linear_packed_bytes(H, Hl) / 2));
-      TRY(fill(tmp, (size_t)H * H, p + "self_attn.o_proj.weight", 0));
+      TRY(fill(tmp, (size_t)H * H, p + "self_attn.o_proj.weight", kres));
       FFMI_HIP(launch_pack_weight(tmp, H, 0, s * Hl, H, Hl, L.wo, 1, 0, H / 16, stream));
       // gate | up: column-parallel, interleaved 16-column tiles
       TRY(alloc(&L.wgu, 2 * ffmi_linear_packed_bytes(Fl, H) / 2));
@@ -519,7 +551,7 @@ struct LlamaGPU : public ffmi_model {
                                   stream));
       // down: row-parallel -> columns [s*Fl, (s+1)*Fl) of [H][F]
       TRY(alloc(&L.wd, ffmi_linear_packed_bytes(H, Fl) / 2));
-      TRY(fill(tmp, (size_t)H * F, p + "mlp.down_proj.weight", 0));
+      TRY(fill(tmp, (size_t)H * F, p + "mlp.down_proj.weight", kres));
       FFMI_HIP(launch_pack_weight(tmp, F, 0, s * Fl, H, Fl, L.wd, 1, 0, H / 16, stream));
       ffmi_attn_cfg ac;
       ac.mode = mode == FFMI_MODEL_TREE ? FFMI_ATTN_TREE
@@ -682,7 +714,11 @@ struct LlamaGPU : public ffmi_model {
       if (st != FFMI_OK) return st;
     }
     FFMI_HIP(hipStreamSynchronize(stream));
-    if (peer && (st = ffmi::comm_status(o.comm)) != FFMI_OK) return st;
+    // any attached transport (also under the RCCL path, whose chunks that fit
+    // the exchange buffer still go over it) reports timeouts / errors here
+    if ((peer || (o.comm && ffmi::comm_peer_attached(o.comm))) &&
+        (st = ffmi::comm_status(o.comm)) != FFMI_OK)
+      return st;
     if (mode == FFMI_MODEL_TREE) tree_parity ^= 1;
     if (!recs.empty()) prof_collect();
     return FFMI_OK;

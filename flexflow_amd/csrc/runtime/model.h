@@ -68,6 +68,12 @@ struct ffmi_model {
     (void)cap;
     return -1;
   }
+  virtual ffmi_status debug_fault(int kind, int layer, int arg) {
+    (void)kind;
+    (void)layer;
+    (void)arg;
+    return FFMI_ERR_UNSUPPORTED;
+  }
   virtual long debug_width(int which) const {
     (void)which;
     return -1;

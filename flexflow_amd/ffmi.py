@@ -30,6 +30,9 @@ X_PACKED = 0x10  # FFMI_X_PACKED flag for the epilogue argument
 Y_PACKED = 0x20  # FFMI_Y_PACKED
 W_STREAM = 0x40  # FFMI_W_STREAM: non-temporal weight loads (speed only)
 F16, F32, I32 = 0, 1, 2
+# synthetic weight inits (ffmi_model_opts.weight_init) and fault kinds
+WEIGHT_INITS = {"uniform": 0, "depth_scaled": 1, "token_chain": 2}
+FAULT_NONE, FAULT_ROPE_POS = 0, 1
 ATTN_QTILE = 32
 MAX_TREE = 64
 
@@ -86,7 +89,7 @@ class ModelOpts(ctypes.Structure):
     _fields_ = [("mode", c_int), ("tp_rank", c_int), ("tp_size", c_int), ("comm", c_void_p),
                 ("max_requests", c_int), ("max_tokens", c_int), ("max_seq_len", c_int),
                 ("max_tree_tokens", c_int), ("weight_seed", c_uint64), ("use_graphs", c_int),
-                ("weights_folder", ctypes.c_char_p)]
+                ("weights_folder", ctypes.c_char_p), ("weight_init", c_int)]
 
 
 class RMConfig(ctypes.Structure):
@@ -162,6 +165,7 @@ SIGNATURES = {
     "ffmi_model_set_debug": (c_int, [c_void_p, c_int]),
     "ffmi_model_debug_tensor": (ctypes.c_long, [c_void_p, c_int, c_int, c_void_p, ctypes.c_long]),
     "ffmi_model_debug_width": (ctypes.c_long, [c_void_p, c_int]),
+    "ffmi_model_debug_fault": (c_int, [c_void_p, c_int, c_int, c_int]),
     "ffmi_set_device": (c_int, [c_int]),
     "ffmi_rm_create": (c_int, [ctypes.POINTER(RMConfig), ctypes.POINTER(c_void_p)]),
     "ffmi_rm_destroy": (None, [c_void_p]),
@@ -184,6 +188,10 @@ SIGNATURES = {
                                 c_float, c_int, c_void_p]),
     "ffmi_pack_activations": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_debug_gemm_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
+    "ffmi_debug_fused_residual_linear": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                                 c_int, c_int, c_void_p]),
+    "ffmi_debug_fused_norm_linear": (c_int, [c_void_p, c_void_p, c_void_p, c_float, c_void_p,
+                                             c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "ffmi_debug_attn_stamps": (ctypes.c_long, [c_void_p, ctypes.c_long]),
     "ffmi_debug_markers": (ctypes.c_long, [c_void_p, ctypes.c_long]),
 }

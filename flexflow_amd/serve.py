@@ -19,16 +19,20 @@ class Model:
 
     def __init__(self, config: dict, mode: str = "inc", *, max_requests=8, max_tokens=128,
                  max_seq_len=512, max_tree_tokens=23, weight_seed=20250117, tp_rank=0,
-                 tp_size=1, comm=None, weights_folder: Optional[str] = None):
+                 tp_size=1, comm=None, weights_folder: Optional[str] = None,
+                 weight_init: Union[int, str] = 0):
         """weights_folder: a checkpoint in the reference's per-tensor format
-        (see checkpoint.convert_hf_model); None: seeded synthetic weights."""
+        (see checkpoint.convert_hf_model); None: seeded synthetic weights,
+        `weight_init` "uniform" (0, the bench's), "depth_scaled" (1) or
+        "token_chain" (2) -- include/ffmi.h ffmi_model_opts."""
         L = F.lib()
         self.config = dict(config)
         self.mode = mode
         cfg = F.LlamaConfig.from_dict(config)
         opts = F.ModelOpts(self.MODES[mode], tp_rank, tp_size, comm.handle if comm else None,
                            max_requests, max_tokens, max_seq_len, max_tree_tokens, weight_seed, 0,
-                           weights_folder.encode() if weights_folder else None)
+                           weights_folder.encode() if weights_folder else None,
+                           F.WEIGHT_INITS.get(weight_init, weight_init))
         h = ctypes.c_void_p()
         F.check(L.ffmi_model_create(ctypes.byref(cfg), ctypes.byref(opts), ctypes.byref(h)),
                 "ffmi_model_create")
@@ -67,6 +71,12 @@ class Model:
         if T < 0:
             raise F.FFMIError(f"debug_tensor({which}, {layer}): nothing captured")
         return buf[:T * width].reshape(T, width).copy()
+
+    def debug_fault(self, kind: int, layer: int = 0, arg: int = 0):
+        """Negative-control fault injection (tests only): F.FAULT_ROPE_POS
+        makes `layer`'s RoPE rotate positions >= arg as position + 1;
+        F.FAULT_NONE clears every fault (include/ffmi.h)."""
+        F.check(F.lib().ffmi_model_debug_fault(self.handle, kind, layer, arg), "debug_fault")
 
     def close(self):
         if getattr(self, "handle", None):
@@ -154,6 +164,12 @@ class Comm:
     def status(self) -> None:
         F.check(F.lib().ffmi_comm_peer_status(self.handle), "peer status")
 
+    def debug_fault(self, kind: int, layer: int = 0, arg: int = 0):
+        """Negative-control fault injection (tests only): F.FAULT_ROPE_POS
+        makes `layer`'s RoPE rotate positions >= arg as position + 1;
+        F.FAULT_NONE clears every fault (include/ffmi.h)."""
+        F.check(F.lib().ffmi_model_debug_fault(self.handle, kind, layer, arg), "debug_fault")
+
     def close(self):
         if getattr(self, "handle", None):
             F.lib().ffmi_comm_destroy(self.handle)
@@ -190,6 +206,12 @@ class RequestManager:
         self.max_sequence_length = max_sequence_length
         self.tokenizer = None
         self._add_special = {}
+
+    def debug_fault(self, kind: int, layer: int = 0, arg: int = 0):
+        """Negative-control fault injection (tests only): F.FAULT_ROPE_POS
+        makes `layer`'s RoPE rotate positions >= arg as position + 1;
+        F.FAULT_NONE clears every fault (include/ffmi.h)."""
+        F.check(F.lib().ffmi_model_debug_fault(self.handle, kind, layer, arg), "debug_fault")
 
     def close(self):
         if getattr(self, "handle", None):

@@ -279,7 +279,11 @@ ffmi_status ffmi_argmax(const void *logits, int T, int V, int32_t *ids,
 /* softmax + ArgTopK (arg_topk.cu:339-448), k <= 4, sorted, lower index on ties */
 ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, int32_t *ids,
                           float *probs, ffmi_stream stream);
-/* seeded synthetic weights, identical to oracle/orc_gen_weight then fp16 */
+/* seeded synthetic weights, identical to oracle/orc_gen_weight then fp16.
+ * kind 0: matrix (uniform, std 0.02); 1: norm weight (1 +- 0.1);
+ * FFMI_WKIND_DEPTH | L: o_proj / down_proj of an L-layer model under the
+ * depth-scaled init (std 0.02 / sqrt(2L)) */
+#define FFMI_WKIND_DEPTH 0x10000
 ffmi_status ffmi_fill_weight(void *dst_f16, size_t n, const char *name,
                              uint64_t seed, int kind, ffmi_stream stream);
 
@@ -324,6 +328,14 @@ typedef struct {
    * K/V projections of GQA checkpoints are replicated to every query head as
    * the reference does (file_loader.cc:292-302).  NULL: synthetic weights. */
   const char *weights_folder;
+  /* synthetic weights (no weights_folder), oracle.h orc_model_create_ex:
+   * 0: every matrix uniform with std 0.02 (the bench's model);
+   * 1: depth-scaled -- o_proj / down_proj at std 0.02 / sqrt(2L);
+   * 2: token chain -- embeddings x 128 and lm_head = the embedding rows
+   *    permuted (v -> (7919 v + 17) mod vocab): a peaked model whose greedy
+   *    picks lead by margins far above fp16 rounding noise (parity tests of
+   *    the reference's literal token bars; SpecInfer with full acceptance) */
+  int weight_init;
 } ffmi_model_opts;
 
 typedef struct ffmi_model ffmi_model;
@@ -381,6 +393,17 @@ int ffmi_model_op_stats(ffmi_model *m, ffmi_op_stat *out, int cap);
 ffmi_status ffmi_model_set_debug(ffmi_model *m, int enable);
 long ffmi_model_debug_tensor(ffmi_model *m, int which, int layer, float *out, long cap);
 long ffmi_model_debug_width(ffmi_model *m, int which);
+/* Negative-control fault injection (tests only; never set in serving): the
+ * parity tests must FAIL on a model with a deliberate bug.
+ *   FFMI_FAULT_ROPE_POS, layer, arg: that layer's RoPE rotates tokens at
+ *     positions >= arg by position + 1 (an off-by-one position in one layer's
+ *     decode phase, apply_rotary_embedding_hf inc_multihead_self_attention.cu:
+ *     664-738 with a wrong abs_depth); layer -1: every layer; arg < 0
+ *     clears it.
+ *   FFMI_FAULT_NONE clears every fault. */
+#define FFMI_FAULT_NONE 0
+#define FFMI_FAULT_ROPE_POS 1
+ffmi_status ffmi_model_debug_fault(ffmi_model *m, int kind, int layer, int arg);
 /* select the HIP device of the calling thread (one process per GPU) */
 ffmi_status ffmi_set_device(int device);
 
@@ -445,6 +468,21 @@ typedef struct {
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 
 
+
+/* Test hooks: the residual RMSNorm folded into the decode GEMMs (T <= 32,
+ * the path of LLaMA-7B decode steps; residual_rms_norm_kernels.cu:98-131
+ * split over the GEMMs around it).  Producer: residual[T][out] += round(X .
+ * W^T) in place (fp16 add) and ss_out[T][out/16] = per 16-column tile sums of
+ * squares of the new residual.  Consumer: Y = (rmsnorm(residual) from ss_in
+ * [T][in/16], weight norm_w, eps) . W^T, with the epilogue (FFMI_EPI_NONE /
+ * FFMI_EPI_SILU_MUL, row-major).  Row-major fp16, no split-K. */
+ffmi_status ffmi_debug_fused_residual_linear(const void *X, const void *W_packed, void *residual,
+                                             float *ss_out, int T, int out_dim, int in_dim,
+                                             ffmi_stream stream);
+ffmi_status ffmi_debug_fused_norm_linear(const void *residual, const float *ss_in,
+                                         const void *norm_w, float eps, const void *W_packed,
+                                         void *Y, int T, int out_dim, int in_dim, int epilogue,
+                                         ffmi_stream stream);
 
 /* Diagnostics: with FFMI_GEMM_STAMP set in the environment, M-split GEMM
  * launches record per-wave timestamps; copies the last launch's records

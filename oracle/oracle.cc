@@ -84,14 +84,36 @@ static inline uint64_t splitmix64(uint64_t z) {
   return z ^ (z >> 31);
 }
 
+// kind 0 / 1 as in oracle.h; kind ORC_WKIND_DEPTH | L: a residual-branch
+// output matrix (o_proj, down_proj) of an L-layer model in the depth-scaled
+// init, amp = 0.02*sqrt(3) / sqrt(2L) (computed here and by the GPU
+// generator's host code with the same float operations)
+extern "C" float orc_weight_amp(int kind) {
+  if (kind == 1) return 0.1f;
+  if (kind & ORC_WKIND_DEPTH) return 0.034641016f / sqrtf((float)(2 * (kind & 0xffff)));
+  return 0.034641016f;  // 0.02*sqrt(3)
+}
+
 extern "C" void orc_gen_weight(const char *name, uint64_t seed, int kind,
                                size_t n, float *out) {
+  orc_gen_weight_rows(name, seed, kind, n, 0, 1, 0, 1.0f, out);
+}
+
+// value i of a [rows][cols] tensor taken from element (perm(r), c) of the
+// stream, perm(r) = (r * pa + pb) mod rows (cols == 0: the identity), the
+// amplitude times `scale` (a power of two in every use: exact)
+extern "C" void orc_gen_weight_rows(const char *name, uint64_t seed, int kind, size_t n,
+                                    int cols, uint64_t pa, uint64_t pb, float scale,
+                                    float *out) {
   const uint64_t key = seed ^ fnv1a64(name);
   const float center = kind == 1 ? 1.0f : 0.0f;
-  const float amp = kind == 1 ? 0.1f : 0.034641016f;  // 0.02*sqrt(3)
+  const float amp = orc_weight_amp(kind) * scale;
+  const uint64_t rows = cols > 0 ? n / cols : 1;
 #pragma omp parallel for schedule(static)
   for (long i = 0; i < (long)n; ++i) {
-    uint64_t x = splitmix64(key + (uint64_t)(i + 1) * 0x9E3779B97F4A7C15ull);
+    uint64_t src = (uint64_t)i;
+    if (cols > 0) src = ((i / cols) * pa + pb) % rows * cols + i % cols;
+    uint64_t x = splitmix64(key + (src + 1) * 0x9E3779B97F4A7C15ull);
     float u = (float)(x >> 40) * (1.0f / 16777216.0f);
     volatile float t = 2.0f * u - 1.0f;  // exact
     volatile float p = t * amp;           // one rounding
@@ -104,7 +126,7 @@ extern "C" void orc_gen_weight(const char *name, uint64_t seed, int kind,
 // ----------------------------------------------------------------------------
 
 // Fixed-order fp32 dot: 8 interleaved partial sums combined pairwise.
-static inline float dot8(const float *a, const float *b, int K) {
+[[maybe_unused]] static inline float dot8(const float *a, const float *b, int K) {
   float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   int k = 0;
   for (; k + 8 <= K; k += 8)
@@ -135,43 +157,178 @@ static inline float dot_ref16(const float *a, const float *b, int K) {
   return acc;
 }
 
-// Summation-order variant of the fp32 dot (orc_set_dot_variant): 0 = dot8
-// (the oracle's order), 1 = dot16 (16 interleaved partial sums, lanes j and
-// j + 8 added before dot8's pairwise combine).  Both are exact fp32
-// restatements of the same sum in different orders; running the model in
-// both measures the drift that ANY change of fp32 summation order produces
-// (the noise floor a GPU/CPU comparison sits on), tests only.
+// Summation-order variants of the fp32 dot (orc_set_dot_variant), tests
+// only: v uses V = 2^v vectors of 8 interleaved partial sums (0 = dot8, the
+// oracle's order; 1 = dot16; 2 = dot32): products k + 8i of each 8V-wide step
+// go to vector i, the V vectors are combined as a pairwise tree, the k < 8V
+// remainder goes on through vector 0, and the 8 lanes combine pairwise.  All
+// are exact fp32 restatements of the same sum in different orders; running
+// the model in several of them measures the drift that ANY change of fp32
+// summation order produces (the noise floor a GPU/CPU comparison sits on).
 static int g_dot_variant = 0;
-extern "C" void orc_set_dot_variant(int v) { g_dot_variant = v == 1 ? 1 : 0; }
+extern "C" void orc_set_dot_variant(int v) { g_dot_variant = v >= 0 && v <= 2 ? v : 0; }
 
-// dot8 of R rows of X against one weight row at once: R independent
-// accumulator chains (the single chain of dot8 is add-latency bound), each
-// with exactly dot8's summation order, so the results are bit-identical.
-template <int R>
-static inline void dot8_rows(const float *const *x, const float *w, int K, float *out) {
-  __m256 acc[R], acc2[R];
-  for (int r = 0; r < R; ++r) acc[r] = acc2[r] = _mm256_setzero_ps();
-  int k = 0;
-  if (g_dot_variant == 1) {
-    for (; k + 16 <= K; k += 16) {
-      const __m256 wv = _mm256_loadu_ps(w + k), wv2 = _mm256_loadu_ps(w + k + 8);
-      for (int r = 0; r < R; ++r) {
-        acc[r] = _mm256_add_ps(acc[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k), wv));
-        acc2[r] = _mm256_add_ps(acc2[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k + 8), wv2));
+// One register tile of the blocked linear: RT activation rows x RN weight
+// rows, V accumulator vectors per output, over k in [k0, k1) (a multiple of
+// 8V steps); accumulators live in acc[t][n][V][8] between k-chunks, so every
+// output still gets exactly its own V x 8 partial sums in k order.
+template <int V, int RT, int RN>
+static inline void lin_tile(const float *X, const float *W, int K, int k0, int k1,
+                            float *acc, int accN) {
+  __m256 a[RT][RN][V];
+  for (int r = 0; r < RT; ++r)
+    for (int j = 0; j < RN; ++j)
+      for (int v = 0; v < V; ++v)
+        a[r][j][v] = _mm256_load_ps(acc + (((size_t)r * accN + j) * V + v) * 8);
+  for (int k = k0; k < k1; k += 8 * V) {
+    for (int v = 0; v < V; ++v) {
+      __m256 x[RT];
+      for (int r = 0; r < RT; ++r) x[r] = _mm256_loadu_ps(X + (size_t)r * K + k + 8 * v);
+      for (int j = 0; j < RN; ++j) {
+        const __m256 w = _mm256_loadu_ps(W + (size_t)j * K + k + 8 * v);
+        for (int r = 0; r < RT; ++r)
+          a[r][j][v] = _mm256_add_ps(a[r][j][v], _mm256_mul_ps(x[r], w));
       }
     }
-    for (int r = 0; r < R; ++r) acc[r] = _mm256_add_ps(acc[r], acc2[r]);
   }
-  for (; k + 8 <= K; k += 8) {
-    const __m256 wv = _mm256_loadu_ps(w + k);
-    for (int r = 0; r < R; ++r)
-      acc[r] = _mm256_add_ps(acc[r], _mm256_mul_ps(_mm256_loadu_ps(x[r] + k), wv));
+  for (int r = 0; r < RT; ++r)
+    for (int j = 0; j < RN; ++j)
+      for (int v = 0; v < V; ++v)
+        _mm256_store_ps(acc + (((size_t)r * accN + j) * V + v) * 8, a[r][j][v]);
+}
+
+// The same tile with AVX-512 (the GPU boxes' EPYC hosts have it; chosen at
+// run time).  Bit-identical: every lane sees the same products added in the
+// same order.  V = 1: a zmm holds the 8-lane sums of TWO activation rows at
+// one weight row (rows r, r+1 in its halves, the weight chunk broadcast);
+// V >= 2: an output's V 8-lane vectors are V/2 zmm of 16 consecutive k.
+template <int V, int RT, int RN>
+__attribute__((target("avx512f,avx512dq"))) static inline void lin_tile512(
+    const float *X, const float *W, int K, int k0, int k1, float *acc, int accN) {
+  if constexpr (V == 1) {
+    static_assert(RT % 2 == 0, "row pairs");
+    constexpr int RP = RT / 2;
+    __m512 a[RP][RN];
+    for (int p = 0; p < RP; ++p)
+      for (int j = 0; j < RN; ++j) {
+        const __m256 lo = _mm256_load_ps(acc + ((size_t)(2 * p) * accN + j) * 8);
+        const __m256 hi = _mm256_load_ps(acc + ((size_t)(2 * p + 1) * accN + j) * 8);
+        a[p][j] = _mm512_insertf32x8(_mm512_castps256_ps512(lo), hi, 1);
+      }
+    for (int k = k0; k < k1; k += 8) {
+      __m512 x[RP];
+      for (int p = 0; p < RP; ++p)
+        x[p] = _mm512_insertf32x8(
+            _mm512_castps256_ps512(_mm256_loadu_ps(X + (size_t)(2 * p) * K + k)),
+            _mm256_loadu_ps(X + (size_t)(2 * p + 1) * K + k), 1);
+      for (int j = 0; j < RN; ++j) {
+        const __m512 w = _mm512_broadcast_f32x8(_mm256_loadu_ps(W + (size_t)j * K + k));
+        for (int p = 0; p < RP; ++p) a[p][j] = _mm512_add_ps(a[p][j], _mm512_mul_ps(x[p], w));
+      }
+    }
+    for (int p = 0; p < RP; ++p)
+      for (int j = 0; j < RN; ++j) {
+        _mm256_store_ps(acc + ((size_t)(2 * p) * accN + j) * 8, _mm512_castps512_ps256(a[p][j]));
+        _mm256_store_ps(acc + ((size_t)(2 * p + 1) * accN + j) * 8,
+                        _mm512_extractf32x8_ps(a[p][j], 1));
+      }
+  } else {
+    constexpr int Z = V / 2;  // zmm per output
+    __m512 a[RT][RN][Z];
+    for (int r = 0; r < RT; ++r)
+      for (int j = 0; j < RN; ++j)
+        for (int z = 0; z < Z; ++z)
+          a[r][j][z] = _mm512_load_ps(acc + (((size_t)r * accN + j) * V + 2 * z) * 8);
+    for (int k = k0; k < k1; k += 8 * V)
+      for (int z = 0; z < Z; ++z) {
+        __m512 x[RT];
+        for (int r = 0; r < RT; ++r) x[r] = _mm512_loadu_ps(X + (size_t)r * K + k + 16 * z);
+        for (int j = 0; j < RN; ++j) {
+          const __m512 w = _mm512_loadu_ps(W + (size_t)j * K + k + 16 * z);
+          for (int r = 0; r < RT; ++r) a[r][j][z] = _mm512_add_ps(a[r][j][z], _mm512_mul_ps(x[r], w));
+        }
+      }
+    for (int r = 0; r < RT; ++r)
+      for (int j = 0; j < RN; ++j)
+        for (int z = 0; z < Z; ++z)
+          _mm512_store_ps(acc + (((size_t)r * accN + j) * V + 2 * z) * 8, a[r][j][z]);
   }
-  for (int r = 0; r < R; ++r) {
-    float s[8];
-    _mm256_storeu_ps(s, acc[r]);
-    for (int kk = k; kk < K; ++kk) s[kk & 7] += x[r][kk] * w[kk];
-    out[r] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+}
+
+static bool has_avx512() {
+  static const int ok = __builtin_cpu_supports("avx512f") && __builtin_cpu_supports("avx512dq") &&
+                        !(getenv("ORC_NO_AVX512") && atoi(getenv("ORC_NO_AVX512")));
+  return ok;
+}
+
+// Blocked Y = X . W^T with the dot order of variant log2(V): threads take
+// blocks of NB weight rows; K is walked in chunks (L1/L2 reuse of both
+// operands), the partial-sum vectors of the block's [T][NB] outputs kept in
+// a per-thread buffer between chunks.
+template <int V>
+static void linear_blocked(const float *X, const float *W, float *Y, int T, int N, int K,
+                           int fp16) {
+  constexpr int NB = 16, KC = 512;
+  constexpr int RT = 3, RN = V == 1 ? 4 : (V == 2 ? 2 : 1);
+  const int Kv = K - K % (8 * V);  // main loop; the rest as in the scalar order
+  const int nblk = (N + NB - 1) / NB;
+  const bool avx = has_avx512();
+#pragma omp parallel
+  {
+    float *acc = (float *)aligned_alloc(64, (size_t)std::max(T, 1) * NB * V * 8 * sizeof(float));
+#pragma omp for schedule(dynamic, 4)
+    for (int b = 0; b < nblk; ++b) {
+      const int n0 = b * NB, nn = std::min(NB, N - n0);
+      memset(acc, 0, (size_t)T * NB * V * 8 * sizeof(float));
+      for (int kc = 0; kc < Kv; kc += KC) {
+        const int k1 = std::min(Kv, kc + KC);
+        int t = 0;
+        if (avx) {  // register tiles of 8 rows (V = 1: 4 row pairs) x 5 / 4 / 2 weight rows
+          constexpr int RT5 = 8, RN5 = V == 1 ? 5 : (V == 2 ? 3 : 1);
+          for (; t + RT5 <= T; t += RT5) {
+            int j = 0;
+            for (; j + RN5 <= nn; j += RN5)
+              lin_tile512<V, RT5, RN5>(X + (size_t)t * K, W + (size_t)(n0 + j) * K, K, kc, k1,
+                                       acc + ((size_t)t * NB + j) * V * 8, NB);
+            for (; j < nn; ++j)
+              lin_tile512<V, RT5, 1>(X + (size_t)t * K, W + (size_t)(n0 + j) * K, K, kc, k1,
+                                     acc + ((size_t)t * NB + j) * V * 8, NB);
+          }
+        }
+        for (; t + RT <= T; t += RT) {
+          int j = 0;
+          for (; j + RN <= nn; j += RN)
+            lin_tile<V, RT, RN>(X + (size_t)t * K, W + (size_t)(n0 + j) * K, K, kc, k1,
+                                acc + ((size_t)t * NB + j) * V * 8, NB);
+          for (; j < nn; ++j)
+            lin_tile<V, RT, 1>(X + (size_t)t * K, W + (size_t)(n0 + j) * K, K, kc, k1,
+                               acc + ((size_t)t * NB + j) * V * 8, NB);
+        }
+        for (; t < T; ++t)
+          for (int j = 0; j < nn; ++j)
+            lin_tile<V, 1, 1>(X + (size_t)t * K, W + (size_t)(n0 + j) * K, K, kc, k1,
+                              acc + ((size_t)t * NB + j) * V * 8, NB);
+      }
+      for (int t = 0; t < T; ++t)
+        for (int j = 0; j < nn; ++j) {
+          const float *av = acc + ((size_t)t * NB + j) * V * 8;
+          const float *x = X + (size_t)t * K, *w = W + (size_t)(n0 + j) * K;
+          __m256 s8 = _mm256_load_ps(av);
+          if (V == 2) s8 = _mm256_add_ps(s8, _mm256_load_ps(av + 8));
+          if (V == 4)
+            s8 = _mm256_add_ps(_mm256_add_ps(s8, _mm256_load_ps(av + 8)),
+                               _mm256_add_ps(_mm256_load_ps(av + 16), _mm256_load_ps(av + 24)));
+          int k = Kv;
+          for (; k + 8 <= K; k += 8)
+            s8 = _mm256_add_ps(s8, _mm256_mul_ps(_mm256_loadu_ps(x + k), _mm256_loadu_ps(w + k)));
+          float s[8];
+          _mm256_storeu_ps(s, s8);
+          for (; k < K; ++k) s[k & 7] += x[k] * w[k];
+          Y[(size_t)t * N + n0 + j] =
+              R(((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7])), fp16);
+        }
+    }
+    free(acc);
   }
 }
 
@@ -185,30 +342,10 @@ extern "C" void orc_linear(const float *X, const float *W, float *Y, int T,
         Y[(size_t)t * N + n] = dot_ref16(X + (size_t)t * K, W + (size_t)n * K, K);
     return;
   }
-  // blocks of 8 weight rows x 4 activation rows: both stay in L2 while the
-  // block is computed (every element still gets its own dot8)
-  constexpr int NB = 8;
-#pragma omp parallel for schedule(static)
-  for (int n0 = 0; n0 < N; n0 += NB) {
-    const int n1 = std::min(N, n0 + NB);
-    float o[4];
-    int t = 0;
-    for (; t + 4 <= T; t += 4) {
-      const float *x[4] = {X + (size_t)t * K, X + (size_t)(t + 1) * K, X + (size_t)(t + 2) * K,
-                           X + (size_t)(t + 3) * K};
-      for (int n = n0; n < n1; ++n) {
-        dot8_rows<4>(x, W + (size_t)n * K, K, o);
-        for (int r = 0; r < 4; ++r) Y[(size_t)(t + r) * N + n] = R(o[r], fp16);
-      }
-    }
-    for (; t < T; ++t) {
-      const float *x[1] = {X + (size_t)t * K};
-      for (int n = n0; n < n1; ++n) {
-        dot8_rows<1>(x, W + (size_t)n * K, K, o);
-        Y[(size_t)t * N + n] = R(o[0], fp16);
-      }
-    }
-  }
+  if (T <= 0 || N <= 0) return;
+  if (g_dot_variant == 1) linear_blocked<2>(X, W, Y, T, N, K, fp16);
+  else if (g_dot_variant == 2) linear_blocked<4>(X, W, Y, T, N, K, fp16);
+  else linear_blocked<1>(X, W, Y, T, N, K, fp16);
 }
 
 static void rms_core(const float *x, const float *w, float *out, int H,
@@ -480,9 +617,9 @@ static void keep_op(orc_model *m, int kind, int layer, const float *src, size_t 
 }
 
 static void gen(fvec &dst, const std::string &name, uint64_t seed,
-                int kind, size_t n, int fp16) {
+                int kind, size_t n, int fp16, int cols = 0, uint64_t pa = 1, float scale = 1.0f) {
   dst.resize(n);
-  orc_gen_weight(name.c_str(), seed, kind, n, dst.data());
+  orc_gen_weight_rows(name.c_str(), seed, kind, n, cols, pa, ORC_CHAIN_B, scale, dst.data());
   if (fp16) {
     float *p = dst.data();
 #pragma omp parallel for schedule(static)
@@ -492,6 +629,11 @@ static void gen(fvec &dst, const std::string &name, uint64_t seed,
 
 extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
                                        int fp16, int max_requests, int max_seq) {
+  return orc_model_create_ex(cfg, seed, fp16, max_requests, max_seq, 0);
+}
+
+extern "C" orc_model *orc_model_create_ex(const orc_config *cfg, uint64_t seed, int fp16,
+                                          int max_requests, int max_seq, int weight_init) {
   if (cfg->num_kv_heads != cfg->num_heads) return nullptr;  // MHA only
   orc_model *m = new orc_model();
   m->c = *cfg;
@@ -500,8 +642,17 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
   m->max_seq = max_seq;
   m->d = cfg->hidden / cfg->num_heads;
   const size_t H = cfg->hidden, F = cfg->intermediate, Vv = cfg->vocab_size;
-  gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16);
-  gen(m->lm, "lm_head.weight", seed, 0, Vv * H, fp16);
+  if (weight_init == 2) {
+    // token-chain init: embeddings x ORC_CHAIN_EMBED_SCALE, lm_head row v =
+    // the unscaled embedding row of perm(v) (a tied, permuted head): the
+    // residual stream keeps the input token's direction, so the logit of
+    // perm^-1(token) leads by a margin far above fp16 rounding noise
+    gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16, 0, 1, ORC_CHAIN_EMBED_SCALE);
+    gen(m->lm, "model.embed_tokens.weight", seed, 0, Vv * H, fp16, (int)H, ORC_CHAIN_A);
+  } else {
+    gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16);
+    gen(m->lm, "lm_head.weight", seed, 0, Vv * H, fp16);
+  }
   gen(m->final_norm, "model.norm.weight", seed, 1, H, fp16);
   m->layers.resize(cfg->num_layers);
   for (int l = 0; l < cfg->num_layers; ++l) {
@@ -512,10 +663,12 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
     gen(L.wq, p + "self_attn.q_proj.weight", seed, 0, H * H, fp16);
     gen(L.wk, p + "self_attn.k_proj.weight", seed, 0, H * H, fp16);
     gen(L.wv, p + "self_attn.v_proj.weight", seed, 0, H * H, fp16);
-    gen(L.wo, p + "self_attn.o_proj.weight", seed, 0, H * H, fp16);
+    // depth-scaled init: the residual-branch outputs at 1/sqrt(2L)
+    const int kres = weight_init == 1 ? (ORC_WKIND_DEPTH | cfg->num_layers) : 0;
+    gen(L.wo, p + "self_attn.o_proj.weight", seed, kres, H * H, fp16);
     gen(L.wg, p + "mlp.gate_proj.weight", seed, 0, F * H, fp16);
     gen(L.wu, p + "mlp.up_proj.weight", seed, 0, F * H, fp16);
-    gen(L.wd, p + "mlp.down_proj.weight", seed, 0, H * F, fp16);
+    gen(L.wd, p + "mlp.down_proj.weight", seed, kres, H * F, fp16);
   }
   m->kc.assign((size_t)max_requests * cfg->num_layers * max_seq * H, 0.f);
   m->vc.assign((size_t)max_requests * cfg->num_layers * max_seq * H, 0.f);
@@ -737,6 +890,97 @@ extern "C" int orc_model_decode_batch(orc_model *m, const int *reqs, const int *
                           d, scale, &att[(size_t)t * H + hd * d], fp16);
       }
     }
+    orc_linear(att.data(), L.wo.data(), o.data(), T, H, H, fp16);
+    orc_residual_rmsnorm(res.data(), o.data(), L.post_norm.data(), r2.data(), h.data(), T, H,
+                         c.rms_eps, fp16);
+    res.swap(r2);
+    orc_linear(h.data(), L.wg.data(), g.data(), T, F, H, fp16);
+    orc_linear(h.data(), L.wu.data(), u.data(), T, F, H, fp16);
+    orc_silu_mul(g.data(), u.data(), a.data(), (size_t)T * F, fp16);
+    orc_linear(a.data(), L.wd.data(), mlp.data(), T, H, F, fp16);
+  }
+  orc_residual_rmsnorm(res.data(), mlp.data(), m->final_norm.data(), r2.data(), h.data(), T, H,
+                       c.rms_eps, fp16);
+  if (logits) orc_linear(h.data(), m->lm.data(), logits, T, c.vocab_size, H, fp16);
+  return 0;
+}
+
+// Several requests' token blocks in one step (the CPU port of a tree-verify
+// or SSM beam step for the cpu_baseline timing): the dense layers run once
+// over all tokens (every weight read once per step, as the GPU step does),
+// attention per request over its cache with causal visibility inside the
+// block -- for a 21-token verify tree or a 3-token beam layer the same work
+// as the reference's bitmask (tree_inc...cu:35-333, spec_inc...cu:36-309).
+extern "C" int orc_model_forward_multi(orc_model *m, int nreq, const int *reqs, const int *counts,
+                                       const int *start, const int *tokens, float *logits) {
+  const orc_config &c = m->c;
+  const int H = c.hidden, F = c.intermediate, d = m->d, nh = c.num_heads;
+  const int fp16 = m->fp16;
+  std::vector<int> off(nreq + 1, 0);
+  for (int r = 0; r < nreq; ++r) {
+    if (reqs[r] < 0 || reqs[r] >= m->max_requests || counts[r] <= 0 ||
+        start[r] + counts[r] > m->max_seq)
+      return -1;
+    off[r + 1] = off[r] + counts[r];
+  }
+  const int T = off[nreq];
+  std::vector<float> res((size_t)T * H), h((size_t)T * H), r2((size_t)T * H);
+  std::vector<float> q((size_t)T * H), k((size_t)T * H), v((size_t)T * H);
+  std::vector<float> att((size_t)T * H), o((size_t)T * H), mlp((size_t)T * H);
+  std::vector<float> g((size_t)T * F), u((size_t)T * F), a((size_t)T * F);
+  for (int t = 0; t < T; ++t)
+    memcpy(&res[(size_t)t * H], &m->emb[(size_t)tokens[t] * H], H * sizeof(float));
+  const float scale = 1.0f / sqrtf((float)d);
+  for (int l = 0; l < c.num_layers; ++l) {
+    auto &L = m->layers[l];
+    if (l == 0) {
+      orc_rmsnorm(res.data(), L.in_norm.data(), h.data(), T, H, c.rms_eps, fp16);
+    } else {
+      orc_residual_rmsnorm(res.data(), mlp.data(), L.in_norm.data(), r2.data(), h.data(), T, H,
+                           c.rms_eps, fp16);
+      res.swap(r2);
+    }
+    orc_linear(h.data(), L.wq.data(), q.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wk.data(), k.data(), T, H, H, fp16);
+    orc_linear(h.data(), L.wv.data(), v.data(), T, H, H, fp16);
+    for (int r = 0; r < nreq; ++r) {
+      float *kc = &m->kc[(((size_t)reqs[r] * c.num_layers + l) * m->max_seq) * H];
+      float *vc = &m->vc[(((size_t)reqs[r] * c.num_layers + l) * m->max_seq) * H];
+      for (int i = 0; i < counts[r]; ++i) {
+        const int t = off[r] + i, pos = start[r] + i;
+        for (int hd = 0; hd < nh; ++hd) {
+          float *qh = &q[(size_t)t * H + hd * d];
+          float *kh = &k[(size_t)t * H + hd * d];
+          rope_apply(qh, d, &m->rope[(size_t)pos * d]);
+          rope_apply(kh, d, &m->rope[(size_t)pos * d]);
+          for (int e = 0; e < d; ++e) {
+            qh[e] = R(qh[e], fp16);
+            kh[e] = R(kh[e], fp16);
+          }
+        }
+        memcpy(kc + (size_t)pos * H, &k[(size_t)t * H], H * sizeof(float));
+        memcpy(vc + (size_t)pos * H, &v[(size_t)t * H], H * sizeof(float));
+      }
+    }
+#pragma omp parallel for collapse(2) schedule(dynamic)
+    for (int r = 0; r < nreq; ++r)
+      for (int hd = 0; hd < nh; ++hd) {
+        const float *kc = &m->kc[(((size_t)reqs[r] * c.num_layers + l) * m->max_seq) * H];
+        const float *vc = &m->vc[(((size_t)reqs[r] * c.num_layers + l) * m->max_seq) * H];
+        const int nk = start[r] + counts[r];
+        std::vector<float> Kh((size_t)nk * d), Vh((size_t)nk * d);
+        std::vector<uint8_t> vis(nk);
+        for (int j = 0; j < nk; ++j) {
+          memcpy(&Kh[(size_t)j * d], kc + (size_t)j * H + hd * d, d * sizeof(float));
+          memcpy(&Vh[(size_t)j * d], vc + (size_t)j * H + hd * d, d * sizeof(float));
+        }
+        for (int i = 0; i < counts[r]; ++i) {
+          const int t = off[r] + i, pos = start[r] + i;
+          for (int j = 0; j < nk; ++j) vis[j] = j <= pos;
+          orc_attention_row(&q[(size_t)t * H + hd * d], Kh.data(), Vh.data(), vis.data(), nk, d,
+                            scale, &att[(size_t)t * H + hd * d], fp16);
+        }
+      }
     orc_linear(att.data(), L.wo.data(), o.data(), T, H, H, fp16);
     orc_residual_rmsnorm(res.data(), o.data(), L.post_norm.data(), r2.data(), h.data(), T, H,
                          c.rms_eps, fp16);

@@ -53,9 +53,23 @@ float orc_round16(float f);
  * value i of tensor `name`: u = top-24 bits of splitmix64(seed ^ fnv1a64(name),
  * i) / 2^24; w = center + (2u-1)*amp, all in fp32, no FMA contraction.
  * kind 0: matrix / embedding (center 0, amp 0.02*sqrt(3)); kind 1: norm
- * weight (center 1, amp 0.1). */
+ * weight (center 1, amp 0.1); kind ORC_WKIND_DEPTH | L: o_proj / down_proj of
+ * an L-layer model in the depth-scaled init (amp 0.02*sqrt(3) / sqrt(2L)). */
+#define ORC_WKIND_DEPTH 0x10000
 void orc_gen_weight(const char *name, uint64_t seed, int kind, size_t n,
                     float *out);
+float orc_weight_amp(int kind);
+/* the same stream as a [n / cols][cols] tensor whose row r is row
+ * (r * pa + pb) mod (n / cols) of the stream (cols == 0: no permutation),
+ * amplitude times `scale` */
+void orc_gen_weight_rows(const char *name, uint64_t seed, int kind, size_t n, int cols,
+                         uint64_t pa, uint64_t pb, float scale, float *out);
+/* token-chain init (weight_init 2): embedding scale and the lm_head row
+ * permutation v -> (v * ORC_CHAIN_A + ORC_CHAIN_B) mod vocab (7919 is prime,
+ * so a bijection for every vocabulary it does not divide) */
+#define ORC_CHAIN_EMBED_SCALE 128.0f
+#define ORC_CHAIN_A 7919u
+#define ORC_CHAIN_B 17u
 
 /* ---- kernel-level restatements ---- */
 /* Linear: Y[T][N] = X[T][K] . W[N][K]^T (linear_kernels.cu:450-582; fp32
@@ -111,6 +125,14 @@ void orc_softmax_topk(const float *logits, int T, int V, int k, int fp16,
 typedef struct orc_model orc_model;
 orc_model *orc_model_create(const orc_config *cfg, uint64_t seed, int fp16,
                             int max_requests, int max_seq);
+/* weight_init 0: every matrix at amp 0.02*sqrt(3) (the bench's model);
+ * 1: depth-scaled -- o_proj / down_proj at 1/sqrt(2L) of that (a residual
+ * stream that does not amplify per-layer rounding; ffmi_model_opts);
+ * 2: token chain -- embeddings x ORC_CHAIN_EMBED_SCALE and lm_head = the
+ * embedding rows permuted (ORC_CHAIN_A/B): a peaked model whose greedy picks
+ * lead by margins far above fp16 rounding noise */
+orc_model *orc_model_create_ex(const orc_config *cfg, uint64_t seed, int fp16,
+                               int max_requests, int max_seq, int weight_init);
 void orc_model_destroy(orc_model *m);
 void orc_model_reset(orc_model *m, int req);
 /* Feed T tokens of request `req` at positions start_pos..start_pos+T-1
@@ -127,6 +149,12 @@ int orc_model_forward_ex(orc_model *m, int req, const int *tokens, int T,
  * dense layers read every weight once for the whole batch. */
 int orc_model_decode_batch(orc_model *m, const int *reqs, const int *tokens,
                            const int *pos, int T, float *logits);
+/* R requests' token blocks in one step: block r = counts[r] tokens of request
+ * reqs[r] at positions start[r].., causal inside the block (the CPU port of a
+ * tree-verify / SSM beam step for the cpu_baseline; dense layers batched over
+ * all tokens).  logits [sum counts][V] or NULL. */
+int orc_model_forward_multi(orc_model *m, int R, const int *reqs, const int *counts,
+                            const int *start, const int *tokens, float *logits);
 /* hidden state (residual stream before final norm) after layer `layer` of
  * the last forward call, [T][H]; layer == num_layers gives final-normed. */
 int orc_model_get_hidden(orc_model *m, int layer, float *out);

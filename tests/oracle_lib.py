@@ -61,6 +61,11 @@ def lib():
         L.orc_model_create.restype = ctypes.c_void_p
         L.orc_model_create.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64,
                                        ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_model_create_ex.restype = ctypes.c_void_p
+        L.orc_model_create_ex.argtypes = [ctypes.POINTER(OrcConfig), ctypes.c_uint64,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+        L.orc_weight_amp.restype = ctypes.c_float
+        L.orc_weight_amp.argtypes = [ctypes.c_int]
         L.orc_model_destroy.argtypes = [ctypes.c_void_p]
         L.orc_model_forward.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
                                         ctypes.c_int, ctypes.c_int, _f32p]
@@ -73,6 +78,8 @@ def lib():
         L.orc_model_decode_batch.argtypes = [ctypes.c_void_p, _i32p, _i32p, _i32p,
                                              ctypes.c_int, _f32p]
         L.orc_model_get_hidden.argtypes = [ctypes.c_void_p, ctypes.c_int, _f32p]
+        L.orc_model_forward_multi.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p, _i32p, _i32p,
+                                              _i32p, _f32p]
         L.orc_model_get_op.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, _f32p]
         L.orc_model_greedy.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
                                        ctypes.c_int, ctypes.c_int, _i32p]
@@ -99,7 +106,8 @@ def set_ref_block(k):
 
 
 def set_dot_variant(v):
-    """0: dot8 (default); 1: dot16 -- another fp32 summation order (noise floor)"""
+    """0: dot8 (default); 1: dot16; 2: dot32 -- other fp32 summation orders of
+    the same sums (the noise floor of GPU-vs-oracle drift)"""
     lib().orc_set_dot_variant(v)
 
 
@@ -203,13 +211,15 @@ def softmax_topk(logits, k, fp16=1):
 class Model:
     """Oracle LLaMA (llama.cc restatement), one KV cache row per request."""
 
-    def __init__(self, cfg, seed, fp16=1, max_requests=4, max_seq=512):
+    def __init__(self, cfg, seed, fp16=1, max_requests=4, max_seq=512, weight_init=0):
         self.cfg = dict(cfg)
         c = OrcConfig(cfg["num_layers"], cfg["vocab_size"], cfg["num_heads"],
                       cfg.get("num_kv_heads", cfg["num_heads"]), cfg["hidden"],
                       cfg["intermediate"], cfg.get("rms_eps", 1e-6),
                       cfg.get("rope_theta", 10000.0))
-        self.h = lib().orc_model_create(ctypes.byref(c), seed, fp16, max_requests, max_seq)
+        # weight_init 1: depth-scaled o/down projections (oracle.h)
+        self.h = lib().orc_model_create_ex(ctypes.byref(c), seed, fp16, max_requests, max_seq,
+                                           int(weight_init))
         if not self.h:
             raise RuntimeError("orc_model_create failed")
         self.fp16 = fp16
@@ -256,6 +266,18 @@ class Model:
         rc = lib().orc_model_decode_batch(self.h, ip(reqs), ip(tokens), ip(pos), T, fp(logits))
         assert rc == 0
         return logits
+
+    def forward_multi(self, reqs, counts, start, tokens, logits=True):
+        """several requests' token blocks in one step (orc_model_forward_multi)"""
+        reqs = np.ascontiguousarray(reqs, np.int32)
+        counts = np.ascontiguousarray(counts, np.int32)
+        start = np.ascontiguousarray(start, np.int32)
+        tokens = np.ascontiguousarray(tokens, np.int32)
+        out = np.empty((int(counts.sum()), self.cfg["vocab_size"]), np.float32) if logits else None
+        rc = lib().orc_model_forward_multi(self.h, len(reqs), ip(reqs), ip(counts), ip(start),
+                                           ip(tokens), fp(out) if logits else None)
+        assert rc == 0
+        return out
 
     def hidden(self, layer, T):
         out = np.empty((T, self.cfg["hidden"]), np.float32)

@@ -1,0 +1,65 @@
+"""The token-parity rule of the GPU tests (test infrastructure).
+
+The reference's own bars (tests/inference/cpp_inference_tests.sh):
+- half precision, free-running: the first 30 tokens of two runs identical
+  (:104-129, :188-189);
+- SpecInfer tokens == incr-decoding tokens (:183-189).
+They compare two FlexFlow runs on trained checkpoints, whose greedy picks lead
+by wide margins.  Here the GPU is compared with the CPU oracle (same rounding
+points, different fp32 summation order) on synthetic weights, so a pick can
+flip where two logits are closer than the reordering noise.  One rule, used by
+every token-level GPU test, decides whether a GPU pick that differs from the
+oracle's is such a tie:
+
+  At the position, teacher-forced (the oracle's logits z0 along the GPU's own
+  sequence; the oracle is T-invariant, so they are the free-running logits
+  while the prefix agrees), the GPU picked g and the oracle o:
+  - ulp: distance of the two tokens' fp16 softmax probabilities; a tie if
+    <= TIE_ULP (the numerical tie of argmax over fp16 probabilities,
+    argmax.cu:62-100 lowest-index rule);
+  - otherwise gap = z0[o] - z0[g] must be <= TIE_SIGMA x sigma_pair, where
+    sigma_pair is the standard deviation of the difference of TWO logits of
+    that row under a change of fp32 summation order: the oracle re-run with
+    its dots reordered (orc_set_dot_variant 1) moves every logit of the row by
+    d_i, and sigma_pair = sqrt(2) x std_i(d_i) (32000 samples of the
+    per-logit noise at that position, not the row maximum).  The pair's own
+    move d_o - d_g is reported beside it.
+  A 3-sigma test: a real kernel bug moves logits by far more than the
+  reordering noise (test_gpu_bench_workload.py's negative control must FAIL
+  this rule).  On shallow models sigma_pair is tiny and the rule reduces to
+  the <= 2-ulp probability tie of test_gpu_e2e.py.
+"""
+import numpy as np
+
+from hip_util import ulp_diff
+
+TIE_ULP = 2
+TIE_SIGMA = 3.0
+
+
+def p16_row(row):
+    p = np.exp(row - row.max())
+    return (p / p.sum()).astype(np.float16)
+
+
+def classify(row0, row1, g, o):
+    """row0: oracle logits at the position; row1: the same with reordered
+    dots (None: no noise estimate, the ulp rule alone)"""
+    p16 = p16_row(row0)
+    out = dict(gpu=int(g), oracle=int(o), ulp=int(ulp_diff(p16[g], p16[o])),
+               gap=float(row0[o] - row0[g]))
+    if row1 is not None:
+        d = (row1 - row0).astype(np.float64)
+        out["sigma_pair"] = float(np.sqrt(2.0) * d.std())
+        out["pair_move"] = float(d[o] - d[g])
+        out["row_max_move"] = float(np.abs(d).max())
+    out["tie"] = bool(out["ulp"] <= TIE_ULP or
+                      ("sigma_pair" in out and out["gap"] <= TIE_SIGMA * out["sigma_pair"]))
+    return out
+
+
+def picks(logits):
+    """the oracle's greedy picks: argmax of fp16 softmax, lowest index"""
+    import oracle_lib as O
+    ids, _ = O.softmax_argmax(np.ascontiguousarray(logits, np.float32), fp16=1)
+    return ids

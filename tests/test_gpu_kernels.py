@@ -233,6 +233,82 @@ def test_rmsnorm_and_residual(T, H):
     close16(out.get(), o_ref, 1, 0.99)
 
 
+def _fused_pair(T, H, Kp, N, epi, seed):
+    """producer (o/down: residual += X . Wp^T, sums of squares) then consumer
+    (qkv or gate/up on the normalised residual) through the test hooks, and
+    the unfused kernels on the same inputs"""
+    rng = np.random.default_rng(seed)
+    X = f16(rng.standard_normal((T, Kp)))
+    Wo = f16(rng.uniform(-0.03, 0.03, (H, Kp)))
+    r0 = f16(rng.standard_normal((T, H)))
+    wn = f16(1 + rng.uniform(-0.1, 0.1, H))
+    eps = 1e-6
+    Wop = packed(Wo)
+    Xb, res = Buf(X), Buf(r0)
+    ss = Buf.empty((T, H // 16), np.float32)
+    F.check(L.ffmi_debug_fused_residual_linear(Xb.ptr, Wop.ptr, res.ptr, ss.ptr, T, H, Kp, None))
+    # unfused producer: the GEMM, then the norm kernel's fp16 residual add
+    Yo = Buf.empty((T, H), np.float16)
+    F.check(L.ffmi_linear(Xb.ptr, Wop.ptr, Yo.ptr, T, H, Kp, F.EPI_NONE, None))
+    r_ref = f16(r0.astype(np.float32) + Yo.get().astype(np.float32))
+    r1 = res.get()
+    assert np.array_equal(r1.view(np.uint16), r_ref.view(np.uint16)), "producer residual"
+    sq = (r1.astype(np.float32) ** 2).reshape(T, H // 16, 16).sum(axis=2)
+    np.testing.assert_allclose(ss.get(), sq, rtol=1e-5, atol=1e-6)
+    # consumer vs the norm kernel + GEMM
+    if epi:
+        Wg = f16(rng.uniform(-0.03, 0.03, (N, H)))
+        Wu = f16(rng.uniform(-0.03, 0.03, (N, H)))
+        gb, ub = Buf(Wg), Buf(Wu)
+        Wq = Buf.empty((L.ffmi_linear_packed_bytes(N, H),), np.uint16)
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, H, Wq.ptr, None))
+    else:
+        Wm = f16(rng.uniform(-0.03, 0.03, (N, H)))
+        Wq = packed(Wm)
+    wb = Buf(wn)
+    Y = Buf.empty((T, N), np.float16)
+    F.check(L.ffmi_debug_fused_norm_linear(res.ptr, ss.ptr, wb.ptr, eps, Wq.ptr, Y.ptr, T, N, H,
+                                           epi, None))
+    hb = Buf.empty((T, H), np.float16)
+    F.check(L.ffmi_rmsnorm(res.ptr, wb.ptr, hb.ptr, T, H, eps, None))
+    Yr = Buf.empty((T, N), np.float16)
+    F.check(L.ffmi_linear(hb.ptr, Wq.ptr, Yr.ptr, T, N, H, epi, None))
+    h_or = O.rmsnorm(r1.astype(np.float32), wn.astype(np.float32), eps)
+    if epi:
+        ref = O.silu_mul(O.linear(h_or, Wg.astype(np.float32)), O.linear(h_or, Wu.astype(np.float32)))
+    else:
+        ref = O.linear(h_or, Wm.astype(np.float32))
+    return Y.get(), Yr.get(), ref
+
+
+@pytest.mark.parametrize("T", [1, 8, 32])
+@pytest.mark.parametrize("N,epi", [(12288, 0), (1024, 0), (11008, 1)])
+def test_fused_residual_norm_gemm_pair_at_7b_width(T, N, epi):
+    """The residual RMSNorm folded into the decode GEMMs (LLaMA-7B decode,
+    H 4096: o/down produce, qkv / gate-up consume), checked at kernel level
+    against the norm kernel + plain GEMM on the same inputs: the producer's
+    residual bit-identical, the consumer within 2 fp16 ulp (3 through the SiLU
+    chain) and >= 99% bit-identical (its rms sums the squares per 16-column
+    tile, then the tiles: an fp32 reordering), and within the same bound of
+    the oracle's rmsnorm + linear."""
+    y, yr, ref = _fused_pair(T, 4096, 4096, N, epi, T * 31 + N)
+    mu = 3 if epi else 2
+    close16(y, yr.astype(np.float32), max_ulp=mu, exact_frac=0.99, atol=1e-3 if epi else None)
+    close16(y, ref, max_ulp=mu, exact_frac=0.98, atol=1e-3 if epi else None)
+
+
+@pytest.mark.parametrize("T", [1, 5, 17, 32])
+@pytest.mark.parametrize("H", [64, 96, 2080])
+def test_fused_norm_consumer_empty_wave_ranges(T, H):
+    """Consumer launches whose waves own no k-step (H 64 / 96: 2-3 k-steps
+    over 4 waves) or a batch plus a tail (H 2080: 65 k-steps over 8 waves):
+    every wave still meets the norm's one barrier (gemm.hip rms_finish) and
+    the results hold the bound above."""
+    y, yr, ref = _fused_pair(T, H, 64, 256, 0, T * 7 + H)
+    close16(y, yr.astype(np.float32), max_ulp=2, exact_frac=0.99)
+    close16(y, ref, max_ulp=2, exact_frac=0.98)
+
+
 # ---------------------------------------------------------------- argmax / topk
 @pytest.mark.parametrize("V", [512, 1000, 1001, 32000])
 def test_softmax_argmax_topk_exact(V):

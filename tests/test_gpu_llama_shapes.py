@@ -9,8 +9,10 @@ Shapes (SURVEY.md §8 constants):
 - LLaMA-65B, TP = 8 per-rank shards (configs D/E): qkv 3072x8192,
   o 8192x1024, gate|up 2x2752x8192, down 8192x2752, lm_head vocab shard
   4000x8192;
-- T = 8 (decode batch, skinny kernel) and T = 168 (8 requests x 21-token
-  verify trees, M-split kernel).
+- T = 8 (decode batch, skinny kernel), T = 168 (8 requests x 21-token
+  verify trees, M-split kernel), T = 577 (the first T with >= 4 row blocks:
+  the fixed prefill plan of gemm.hip mid_plan) and T = 1024 (bench.py's
+  prefill step: 8 prompts x 128 tokens, max_tokens_per_batch 1024).
 Tolerance as test_gpu_kernels.close16: <= 2 fp16 ulp (or 1e-4 * max |ref|)
 everywhere and >= 99% of elements bit-identical (only the fp32 summation
 order differs).
@@ -36,7 +38,7 @@ SHAPES = {
 }
 
 
-@pytest.mark.parametrize("T", [8, 168])
+@pytest.mark.parametrize("T", [8, 168, 577, 1024])
 @pytest.mark.parametrize("shape", list(SHAPES))
 def test_linear_at_baseline_shapes(shape, T):
     N, K, epi = SHAPES[shape]

@@ -141,3 +141,22 @@ def test_oracle_ref16_within_half_tolerance(tag):
     bad = np.abs(logits - g["logits"]) > 1e-2
     assert bad.mean() <= 0.05
     assert not np.array_equal(logits, O.Model(cfg, cfg["seed"], fp16=1).forward(0, g["prompt"], 0))
+
+
+def test_oracle_forward_multi_equals_per_request_forwards():
+    """orc_model_forward_multi (the CPU port of a verify / beam step used by
+    bench.py's cpu_baseline) batches the dense layers over several requests'
+    blocks: bit-identical to one orc_model_forward per request."""
+    cfg = dict(num_layers=2, vocab_size=500, num_heads=4, num_kv_heads=4, hidden=128,
+               intermediate=256, rms_eps=1e-6, rope_theta=10000.0)
+    a = O.Model(cfg, 3, fp16=1, max_requests=3, max_seq=64)
+    b = O.Model(cfg, 3, fp16=1, max_requests=3, max_seq=64)
+    rng = np.random.default_rng(0)
+    prompts = [rng.integers(3, 500, size=n).astype(np.int32) for n in (9, 14, 5)]
+    for r, p in enumerate(prompts):
+        a.forward(r, p, 0)
+        b.forward(r, p, 0)
+    blocks = [rng.integers(3, 500, size=n).astype(np.int32) for n in (3, 1, 6)]
+    ref = np.vstack([a.forward(r, blk, len(prompts[r])) for r, blk in enumerate(blocks)])
+    got = b.forward_multi([0, 1, 2], [3, 1, 6], [len(p) for p in prompts], np.concatenate(blocks))
+    assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
