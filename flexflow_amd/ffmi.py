@@ -8,7 +8,7 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 # FFMI_LIB_VARIANT=<suffix> loads libffmi_<suffix>.so from the same directory
-# (build-flag A/B runs, e.g. scripts/gpu_lib_ab.sh); the default is libffmi.so
+# (build-flag A/B runs, e.g. scripts/gpu_ab.sh "" FFMI_LIB_VARIANT=x); the default is libffmi.so
 _VARIANT = os.environ.get("FFMI_LIB_VARIANT", "")
 LIB_PATH = os.path.join(_HERE, f"libffmi_{_VARIANT}.so" if _VARIANT else "libffmi.so")
 

@@ -108,3 +108,46 @@ def vshard_task(fa, comm, rank, n, T, V, k, seed):
         ri, rp = O.softmax_topk(x.astype(np.float32), k, fp16=1)
         out["ref_ids"], out["ref_probs"] = ri.reshape(T, k), rp.reshape(T, k)
     return out
+
+
+def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ssm_cfg,
+                     tf_seqs=(), weight_init=0):
+    """One TP shard per rank of a full-depth model over the xGMI transport:
+    incr decoding (spec False) or SpecInfer with the SSM replicated on every
+    rank (spec_infer.cc:385-387).  Then, in incr mode, a teacher-forced pass:
+    the sequences `tf_seqs` (+ this run's own) as ONE prefill step with the
+    logits captured (this rank's vocab shard, [T][V/n]); the row predicting
+    token j + 1 of sequence s is s's j-th row of its block."""
+    B = len(prompts)
+    mtb = 256
+    if spec:
+        extra = 23 * B
+        m = fa.Model(cfg, "tree", max_requests=B, max_tokens=mtb + extra, max_seq_len=128,
+                     weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm,
+                     weight_init=weight_init)
+        ssm = fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=mtb + extra, max_seq_len=128,
+                       max_tree_tokens=23, weight_seed=68, weight_init=weight_init)
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=128, spec_tree_width=(1, 1, 3))
+        rm.register_ssm_model(ssm)
+        res = fa.generate(rm, m, prompts, max_length=max_length, spec=True)
+        out = {"tokens": [r.output_tokens for r in res], "llm_steps": rm.stats().llm_steps}
+        m.close()
+        ssm.close()
+        return out
+    nt = B + len(tf_seqs)
+    m = fa.Model(cfg, "inc", max_requests=max(B, nt), max_tokens=2 * mtb, max_seq_len=128,
+                 weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm, weight_init=weight_init)
+    rm = fa.RequestManager(max_requests_per_batch=max(B, nt), max_tokens_per_batch=mtb,
+                           max_sequence_length=128)
+    res = fa.generate(rm, m, prompts, max_length=max_length)
+    toks = [r.output_tokens for r in res]
+    seqs = list(tf_seqs) + toks
+    assert sum(len(s) for s in seqs) <= 2 * mtb and len(set(map(len, seqs))) == 1
+    m.set_debug(True)
+    fa.generate(fa.RequestManager(max_requests_per_batch=nt, max_tokens_per_batch=2 * mtb,
+                                  max_sequence_length=128), m, [s[1:] for s in seqs],
+                max_length=len(seqs[0]) + 1)
+    lg = m.debug_tensor("logits")
+    m.close()
+    return {"tokens": toks, "tf_logits": lg.astype(np.float16), "tf_seqs": seqs}

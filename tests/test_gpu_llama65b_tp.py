@@ -1,0 +1,138 @@
+"""Configs D and E at full size on one MI355X: LLaMA-65B (80 layers, H 8192,
+64 heads of 128, FFN 22016, vocab 32000; 130 GB of fp16 weights, which fit the
+288 GB of one MI355X) at TP = 1 against the same model sharded over 8 rank
+PROCESSES (TP = 8, the driver's 8-GPU layout: heads and FFN columns sharded,
+o/down row-parallel with all-reduces over the direct xGMI transport, the
+vocab-sharded lm_head tail, graphed steps), the shards time-sharing device 0
+(tests/peer_group.py).  The reference's TP-invariance check
+(tests/inference/cpp_inference_tests.sh:203-217: different TP degrees give the
+same tokens) in incremental decoding and in SpecInfer with the LLaMA-68M SSM
+replicated per rank (spec_infer.cc:385-387), 3 prompts, 32 new tokens.
+
+Rule (parity_rules.py): tokens identical, or every differing pick a tie by
+the 3-sigma test of the two competing logits -- here the "reordered run" is
+the other TP degree itself: both degrees are teacher-forced along the TP = 8
+sequences in one prefill step each, TP = 1's logits pick, and the per-logit
+TP = 8 - TP = 1 difference of that row gives sigma_pair (an 80-layer
+random-weight model: the fp32 partitioning of TP moves the logits like any
+reordering; there is no 65B oracle -- 260 GB of fp32 on the host).
+In the token-chain init (test_gpu_token_chain.py) the margins leave no ties:
+identical tokens demanded literally, and SpecInfer accepts whole trees.
+"""
+import time
+
+import numpy as np
+import pytest
+
+import flexflow_amd as fa
+import peer_tasks as PT
+from hip_util import report
+from parity_rules import classify, picks
+from peer_group import run_group
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
+
+LLAMA_65B = dict(num_layers=80, vocab_size=32000, num_heads=64, num_kv_heads=64, hidden=8192,
+                 intermediate=22016, rms_eps=1e-5, rope_theta=10000.0)
+LLAMA_68M = dict(num_layers=2, vocab_size=32000, num_heads=12, num_kv_heads=12, hidden=768,
+                 intermediate=3072, rms_eps=1e-6, rope_theta=10000.0)
+SEED = 20250117
+NEW = 32
+TP = 8
+
+
+def prompts():
+    rng = np.random.default_rng(6565)
+    return [rng.integers(3, 32000, size=12).tolist() for _ in range(3)]
+
+
+def tp1_run(ps, max_length, tf_seqs, weight_init):
+    """TP = 1 in this process: SpecInfer, then incr decoding + the teacher-
+    forced step over tf_seqs (one prefill, logits [T][V])"""
+    B = len(ps)
+    tree = fa.Model(LLAMA_65B, "tree", max_requests=B, max_tokens=256 + 23 * B, max_seq_len=128,
+                    weight_seed=SEED, weight_init=weight_init)
+    ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=256 + 23 * B, max_seq_len=128,
+                   max_tree_tokens=23, weight_seed=68, weight_init=weight_init)
+    rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=256,
+                           max_sequence_length=128, spec_tree_width=(1, 1, 3))
+    rm.register_ssm_model(ssm)
+    spec = [r.output_tokens for r in fa.generate(rm, tree, ps, max_length=max_length, spec=True)]
+    spec_steps = rm.stats().llm_steps
+    tree.close()
+    ssm.close()
+    nt = len(tf_seqs)
+    m = fa.Model(LLAMA_65B, "inc", max_requests=max(B, nt), max_tokens=512, max_seq_len=128,
+                 weight_seed=SEED, weight_init=weight_init)
+    rmi = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=256,
+                            max_sequence_length=128)
+    incr = [r.output_tokens for r in fa.generate(rmi, m, ps, max_length=max_length)]
+    incr_steps = rmi.stats().llm_steps
+    m.set_debug(True)
+    fa.generate(fa.RequestManager(max_requests_per_batch=nt, max_tokens_per_batch=512,
+                                  max_sequence_length=128), m, [s[1:] for s in tf_seqs],
+                max_length=len(tf_seqs[0]) + 1)
+    lg = m.debug_tensor("logits")
+    m.close()
+    return dict(spec=spec, incr=incr, tf_logits=lg, spec_steps=spec_steps, incr_steps=incr_steps)
+
+
+def judge(seqs, n_prompts, lg1, lg8, L):
+    """every pick of each teacher-forced sequence vs TP = 1's argmax, ties by
+    the rule with TP = 8's row as the reordered run"""
+    verdicts, exact, total = [], 0, 0
+    for s, (seq, n_prompt) in enumerate(zip(seqs, n_prompts)):
+        rows = slice(s * L + n_prompt - 1, s * L + L - 1)
+        z1, z8 = lg1[rows].astype(np.float32), lg8[rows].astype(np.float32)
+        gen = np.array(seq[n_prompt:])
+        ids = picks(z1)
+        for t in np.nonzero(ids != gen)[0]:
+            verdicts.append(dict(seq=s, pos=int(t), **classify(z1[t], z8[t], gen[t], ids[t])))
+        exact += int((ids == gen).sum())
+        total += len(gen)
+    return verdicts, exact, total
+
+
+@pytest.mark.parametrize("weight_init", ["uniform", "token_chain"])
+def test_llama65b_80L_tp8_processes_vs_tp1(weight_init):
+    ps = prompts()
+    n_prompts = [len(p) + 1 for p in ps]
+    max_length = n_prompts[0] + NEW
+    t0 = time.time()
+    # TP = 8: SpecInfer, then incr decoding with the teacher-forced step over
+    # both runs' sequences
+    spec8 = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, True, LLAMA_68M,
+                                                (), weight_init),
+                      max_bytes=(512 + 23 * 3 + 16) * 8192 * 2, timeout=900)
+    s8spec = spec8[0]["tokens"]
+    inc8 = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, False, LLAMA_68M,
+                                               tuple(s8spec), weight_init),
+                     max_bytes=(512 + 23 * 3 + 16) * 8192 * 2, timeout=900)
+    for r in range(TP):
+        assert spec8[r]["tokens"] == s8spec and inc8[r]["tokens"] == inc8[0]["tokens"], r
+    s8 = inc8[0]["tokens"]
+    tf_seqs = inc8[0]["tf_seqs"]  # [spec8 sequences..., incr8 sequences...]
+    lg8 = np.concatenate([inc8[r]["tf_logits"] for r in range(TP)], axis=1)  # vocab shards
+    t8 = time.time() - t0
+    # TP = 1 (the TP = 8 ranks have exited: their 130 GB are free again)
+    one = tp1_run(ps, max_length, tf_seqs, weight_init)
+    L = max_length
+    assert lg8.shape == one["tf_logits"].shape == (len(tf_seqs) * L, 32000)
+    nps = n_prompts + n_prompts
+    verdicts, exact, total = judge(tf_seqs, nps, one["tf_logits"], lg8, L)
+    same = dict(incr_tp8_eq_tp1=sum(a == b for a, b in zip(s8, one["incr"])),
+                spec_tp8_eq_tp1=sum(a == b for a, b in zip(s8spec, one["spec"])),
+                tp8_spec_eq_incr=sum(a == b for a, b in zip(s8spec, s8)),
+                tp1_spec_eq_incr=sum(a == b for a, b in zip(one["spec"], one["incr"])))
+    report(f"llama65b_80L_tp8_vs_tp1_{weight_init}", requests=len(ps), new_tokens=NEW,
+           mismatches_vs_tp1=verdicts, exact=exact, total=total, tp8_seconds=round(t8, 1),
+           incr_steps=one["incr_steps"], spec_steps=one["spec_steps"],
+           tp8_spec_steps=spec8[0]["llm_steps"], **same)
+    if weight_init == "token_chain":  # literal bars
+        assert s8 == one["incr"] == s8spec == one["spec"], same
+        assert not verdicts, verdicts
+        assert one["incr_steps"] >= 1.5 * one["spec_steps"], (one["incr_steps"], one["spec_steps"])
+    else:
+        assert all(v["tie"] for v in verdicts), [v for v in verdicts if not v["tie"]]
+        # the TP = 1 runs themselves: identical to TP = 8, or separated at a tie
+        # of the TP = 8 sequences' teacher-forced rows (checked above)

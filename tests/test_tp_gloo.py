@@ -7,11 +7,18 @@ model.cc:3421-3445):
   * o_proj row-parallel:            columns [s*Hl, (s+1)*Hl), then all-reduce;
   * gate/up column-parallel:        rows [s*Fl, (s+1)*Fl);
   * down_proj row-parallel:         columns [s*Fl, (s+1)*Fl), then all-reduce;
-  * norms, residuals, embedding and lm_head replicated.
+  * norms, residuals and embedding replicated;
+  * lm_head vocab-sharded (model.cc:3392-3419): rank s holds rows
+    [s*Vl, (s+1)*Vl) and the greedy / speculative tail is the sharded softmax
+    top-k of ffmi_vocab_shard_topk -- three exchanges (global max; sum of
+    exp against it, in double; each shard's top-k candidates with global
+    ids), then the merge by fp16 probability with the lowest-index tie rule.
 Here each rank runs that decomposition with the oracle's per-op kernels
-(fp32 semantics) and torch.distributed.all_reduce, and rank 0's logits must
-match the HF golden fixture of the unsharded model.  A second test runs the
-bench's multi-rank control plane (bench.Ctrl) with two processes.
+(fp32 semantics) and torch.distributed collectives: the gathered logit
+shards must match the HF golden fixture of the unsharded model, and every
+rank's merged top-k must equal the oracle's softmax top-k of the full row.
+A second test runs the bench's multi-rank control plane (bench.Ctrl) with
+two processes.
 """
 import os
 import socket
@@ -95,8 +102,36 @@ def _tp_forward(rank, world, tag, out_path, port):
             dn = allreduce(O.linear(a, wd, 0))
             x = x + dn
         xf = O.rmsnorm(x, O.gen_weight("model.norm.weight", seed, 1, H), eps, 0)
-        logits = O.linear(xf, W("lm_head.weight", V, H), 0)
-        np.save(out_path.format(rank=rank), logits)
+        Vl = V // world
+        lg = O.linear(xf, W("lm_head.weight", V, H)[s * Vl:(s + 1) * Vl], 0)  # [T][Vl]
+        # sharded softmax top-k (ffmi_vocab_shard_topk): 1) global max
+        mx = torch.from_numpy(lg.max(axis=1).astype(np.float32))
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        M = mx.numpy()
+        # 2) sum of exp against the global max, double, summed over shards
+        e = np.exp((lg - M[:, None]).astype(np.float32)).astype(np.float32)
+        sm = torch.from_numpy(e.astype(np.float64).sum(axis=1))
+        dist.all_reduce(sm)
+        S = sm.numpy().astype(np.float32)
+        # 3) each shard's top-k candidates (fp16 probability, lowest index)
+        k = 3
+        p16 = (e / S[:, None]).astype(np.float16).astype(np.float32)
+        gid = np.arange(Vl) + s * Vl
+        cand = np.zeros((T, k, 2), np.float32)
+        for t in range(T):
+            order = np.lexsort((gid, -p16[t]))[:k]
+            cand[t, :, 0], cand[t, :, 1] = p16[t, order], gid[order]
+        allc = [torch.zeros_like(torch.from_numpy(cand)) for _ in range(world)]
+        dist.all_gather(allc, torch.from_numpy(cand))
+        allc = np.concatenate([a.numpy() for a in allc], axis=1)  # [T][world*k][2]
+        top = np.zeros((T, k), np.int64)
+        for t in range(T):
+            order = np.lexsort((allc[t, :, 1], -allc[t, :, 0]))[:k]
+            top[t] = allc[t, order, 1].astype(np.int64)
+        shards = [torch.zeros_like(torch.from_numpy(lg)) for _ in range(world)]
+        dist.all_gather(shards, torch.from_numpy(np.ascontiguousarray(lg)))
+        np.save(out_path.format(rank=rank), np.concatenate([x.numpy() for x in shards], axis=1))
+        np.save(out_path.format(rank=rank) + ".top.npy", top)
     finally:
         dist.destroy_process_group()
 
@@ -121,9 +156,13 @@ def test_tp2_decomposition_matches_unsharded_golden(tag, tmp_path):
     _run_ranks([tag, out, str(_free_port())])
     _, g = O.load_golden(tag)
     l0, l1 = np.load(out.format(rank=0)), np.load(out.format(rank=1))
-    np.testing.assert_array_equal(l0, l1)  # replicated tail: ranks agree exactly
+    np.testing.assert_array_equal(l0, l1)  # the gathered shards: ranks agree exactly
     np.testing.assert_allclose(l0, g["logits"], rtol=1e-4, atol=5e-5)
     assert (l0.argmax(-1) == g["logits"].argmax(-1)).all()
+    # the sharded top-k merge equals the unsharded softmax top-k, on every rank
+    ids, _ = O.softmax_topk(l0, 3, fp16=1)
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(out.format(rank=r) + ".top.npy"), ids)
 
 
 _CTRL_CHILD = r"""
