@@ -175,36 +175,70 @@ def run_generate(rm, llm, prompts, max_length, spec):
     return new, lat, res
 
 
-def cpu_baseline(prompt_len=128, max_steps=128, budget_s=15.0, batch=8):
-    """The CPU restatement (oracle/, test infrastructure) timed on the host:
-    LLaMA-7B fp16-semantics incremental decoding, batch 8, batched decode
-    steps at the GPU run's decode positions (prompt_len, prompt_len + 1, ...)
-    until ~budget_s of CPU work (a bounded sample of the workload).  The
-    128-token prefill itself is not run -- at ~7 TMAC it alone would take
-    minutes on the host -- so the first prompt_len KV-cache rows hold zeros:
-    a timing sample (the attention reads the same number of keys as the GPU
-    run's decode steps), not a token-exact replay."""
+def cpu_baseline(acceptance=1.0, prompt_len=128, batch=8, budget_s=12.0, incr_budget_s=8.0):
+    """The CPU restatement (oracle/, test infrastructure) timed on the host,
+    on a bounded sample of the same workload (the headline's metric first):
+    - SpecInfer: LLaMA-7B verify steps (8 requests x 21-token trees at the
+      GPU run's decode positions 128+: 168 tokens per step, the dense layers
+      batched over them, orc_model_forward_multi) and, per verify, the
+      LLaMA-68M SSM's 8 beam steps (tree layers of 1, 1, 3, ... tokens per
+      request, widths (1,1,3)); tokens/s = batch x acceptance / (verify + its
+      8 SSM steps), with the GPU run's own measured acceptance (tokens
+      committed per request per verify), so both sides decode at the same
+      rate of tokens per step;
+    - incremental decoding: batched T = 8 decode steps (orc_model_decode_batch).
+    The 128-token prefill is not run (~7 TMAC, minutes on the host): the
+    first prompt_len KV rows hold zeros, so this is a timing sample (every
+    step reads as many keys as the GPU run's), not a token replay."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
 
     import oracle_lib as O
-    m = O.Model(LLAMA_7B, 20250117, fp16=1, max_requests=batch,
-                max_seq=prompt_len + max_steps + 2)
-    prompts = make_prompts(batch, 1, LLAMA_7B["vocab_size"], seed=7)
-    reqs = np.arange(batch, dtype=np.int32)
-    toks = [pr[-1] for pr in prompts]
+    tree = 21  # 1 root + layers 1, 1, 3 x 6 (widths (1,1,3), 8 SSM steps)
+    layer_sizes = [1, 1, 3, 3, 3, 3, 3, 3]
+    m = O.Model(LLAMA_7B, 20250117, fp16=1, max_requests=batch, max_seq=prompt_len + 160)
+    ssm = O.Model(LLAMA_68M, 68, fp16=1, max_requests=batch, max_seq=prompt_len + 160)
+    g = splitmix64_stream(7)
+    rnd = lambda n: [3 + next(g) % (LLAMA_7B["vocab_size"] - 3) for _ in range(n)]  # noqa: E731
+    reqs = list(range(batch))
+    t_verify, t_ssm, steps = 0.0, 0.0, 0
     t0 = time.time()
-    steps = 0
-    while steps < max_steps and time.time() - t0 < budget_s:
-        logits = m.decode_batch(reqs, toks, [prompt_len + steps] * batch)
-        toks = O.softmax_argmax(logits, fp16=1)[0].tolist()
+    while time.time() - t0 < budget_s and steps < 8:
+        pos = prompt_len + steps  # one committed token per request per step
+        t1 = time.time()
+        depth = 0
+        for k in layer_sizes:  # the SSM's beam steps build the tree layer by layer
+            ssm.forward_multi(reqs, [k] * batch, [pos + depth] * batch, rnd(k * batch))
+            depth += k
+        t2 = time.time()
+        m.forward_multi(reqs, [tree] * batch, [pos] * batch, rnd(tree * batch))
+        t3 = time.time()
+        t_ssm += t2 - t1
+        t_verify += t3 - t2
         steps += 1
-    dt = time.time() - t0
-    return dict(value=round(batch * steps / dt, 3), unit="decoded tokens/s",
+    spec = batch * acceptance * steps / (t_verify + t_ssm)
+    # incremental decoding leg
+    toks = rnd(batch)
+    t0 = time.time()
+    isteps = 0
+    while isteps < 64 and time.time() - t0 < incr_budget_s:
+        logits = m.decode_batch(reqs, toks, [prompt_len + isteps] * batch)
+        toks = O.softmax_argmax(logits, fp16=1)[0].tolist()
+        isteps += 1
+    dti = time.time() - t0
+    return dict(value=round(spec, 3), unit="decoded tokens/s",
                 cores=int(O.lib().orc_num_threads()), kind="port",
-                sample=f"oracle LLaMA-7B incr decoding, batch {batch}, {steps} decode steps at "
-                       f"positions {prompt_len}-{prompt_len + steps - 1} (the GPU run's decode "
-                       f"range; prefill rows zero-filled, not computed), {dt:.1f}s")
+                sample=(f"oracle LLaMA-7B SpecInfer with the LLaMA-68M SSM, batch {batch}: {steps} "
+                        f"verify steps (168 tree tokens at positions {prompt_len}+) + "
+                        f"{8 * steps} SSM beam steps, {t_verify + t_ssm:.1f}s "
+                        f"(verify {t_verify / steps:.2f}s, SSM {t_ssm / (8 * steps) * 1e3:.1f}ms "
+                        f"per step), at the GPU run's acceptance {acceptance:.3f} tokens per "
+                        f"request per verify; prefill rows zero-filled, not computed"),
+                verify_step_s=round(t_verify / steps, 3),
+                ssm_step_ms=round(t_ssm / (8 * steps) * 1e3, 2),
+                incr_decoding={"value": round(batch * isteps / dti, 3), "unit": "decoded tokens/s",
+                               "sample": f"{isteps} batched decode steps at positions "
+                                         f"{prompt_len}-{prompt_len + isteps - 1}, {dti:.1f}s"})
 
 
 def pmc_traffic(kernel):
@@ -547,7 +581,8 @@ def main():
                                 "llm_steps": rmi.stats().llm_steps}
         inc.close()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline()
+        out["cpu_baseline"] = cpu_baseline(
+            acceptance=out.get("tokens_per_request_verify", 1.0) if spec else 1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
     llm.close()
