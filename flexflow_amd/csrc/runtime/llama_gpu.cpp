@@ -73,7 +73,8 @@ struct LlamaGPU : public ffmi_model {
   // residual norms folded into the skinny GEMMs around them (T <= 32, TP = 1):
   // per-tile sums of squares of the residual after o (ss_o) and after down
   // (ss_d), [32][H/16] each.  Only where o/down run unsplit anyway (H/16 >=
-  // 128 tiles: LLaMA-7B decode, 2414 -> 2474-2488 tokens/s); the 68M SSM's
+  // 128 tiles: LLaMA-7B decode, +1.9% incr decoding -- the A/B of record is
+  // profiles/r03_fused_norm_ab.log, quoted in DESIGN.md §5); the 68M SSM's
   // o/down split K over workgroups, and unsplitting them to fuse cost more
   // than the norm launches saved (SSM step +4 us).  FFMI_FUSE_NORM: 0 off,
   // 1 auto (default), 2 every width (tests)
