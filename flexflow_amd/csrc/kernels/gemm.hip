@@ -1129,7 +1129,7 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
 struct WidePlan {
   int NTW, S;
 };
-static WidePlan wide_plan(int T, int N, int K, int epi) {
+static WidePlan wide_plan(int T, int N, int K, int epi, int max_s = 8) {
   WidePlan p{0, 0};
   const int mtiles = (T + 15) / 16;
   if (mtiles <= 8 || mtiles > 12) return p;
@@ -1156,7 +1156,7 @@ static WidePlan wide_plan(int T, int N, int K, int epi) {
   for (int ntw : {12, 16}) {
     const int nblk = (ntiles + ntw - 1) / ntw;
     int S = std::max(1, 256 / nblk);
-    S = std::min(S, std::min(8, std::max(1, KT / 8)));
+    S = std::min(S, std::min(max_s, std::max(1, KT / 8)));
     if (epi) S = std::min(S, 2);
     if (nblk * S < 192) continue;
     return WidePlan{ntw, S};
@@ -1174,7 +1174,8 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
   const int S = std::max(std::max(mid_plan(T, N, K, epilogue, false).S,
                                   epilogue ? 1 : mid_plan(T, N, K, epilogue, true).S),
-                         wide_plan(T, N, K, epilogue).S);
+                         std::max(wide_plan(T, N, K, epilogue).S,
+                                  epilogue ? 1 : wide_plan(T, N, K, epilogue, 16).S));
   return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
 }
 
@@ -1289,8 +1290,10 @@ static hipError_t run_wide(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, f
                                         ws, Y, T, N, ntiles, S, yp);
     else if (S <= 4) hipLaunchKernelGGL((gemm_reduce_kernel<0, 4>), dim3(blocks), dim3(256), 0, s,
                                         ws, Y, T, N, ntiles, S, yp);
-    else hipLaunchKernelGGL((gemm_reduce_kernel<0, 8>), dim3(blocks), dim3(256), 0, s, ws, Y, T, N,
-                            ntiles, S, yp);
+    else if (S <= 8) hipLaunchKernelGGL((gemm_reduce_kernel<0, 8>), dim3(blocks), dim3(256), 0, s,
+                                        ws, Y, T, N, ntiles, S, yp);
+    else hipLaunchKernelGGL((gemm_reduce_kernel<0, 16>), dim3(blocks), dim3(256), 0, s, ws, Y, T,
+                            N, ntiles, S, yp);
   }
   return hipGetLastError();
 }
@@ -1344,7 +1347,7 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
 #undef FFMI_FZ
   }
   if (mtiles > 8 && mtiles <= 12 && xp) {
-    const WidePlan w = wide_plan(T, N, K, epilogue);
+    const WidePlan w = wide_plan(T, N, K, epilogue, defer ? defer->max_s : 8);
     if (w.NTW) {
 #define FFMI_WRUN(NW) \
   return run_wide<NW>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, yp, w.S, defer, nt, wpitch)
