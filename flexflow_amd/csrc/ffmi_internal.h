@@ -115,10 +115,6 @@ __device__ __forceinline__ BatchView batch_view(const char *blob) {
 struct Partials {
   const float *p = nullptr;
   int S = 0, NP = 0;
-  // input to launch_gemm: the most slabs the caller's consumer combines (the
-  // residual norm: 16 at H <= 4096; the all-reduce copy-in and the attention
-  // prologue: 8)
-  int max_s = 8;
 };
 __device__ __forceinline__ float partials_value(const float *p, int S, int NP, int T, int t,
                                                 int n) {

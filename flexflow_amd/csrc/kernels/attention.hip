@@ -101,8 +101,7 @@ __device__ __forceinline__ void st_h4(uint16_t *p, uint16_t a, uint16_t b, uint1
 // loads are back, before the first store.
 // PSRC: 1 = qkv from split-K slabs, 0 = fp16 qkv, -1 = decided at run time
 // by `part` (a compile-time source keeps the two load paths from joining:
-// the join's register copies waited for half of the slab loads); 2 = slabs,
-// up to four of them in the first round trip (the wide GEMM's 4-slice qkv).
+// the join's register copies waited for half of the slab loads).
 template <int D, int NQ, int NT, int PSRC = -1, class AfterLoads, class BeforeStores>
 __device__ __forceinline__ void kv_update_item(
     const BatchView &bv, const WorkDev *__restrict__ wdp, int h, int heads, int slots, int T,
@@ -117,8 +116,6 @@ __device__ __forceinline__ void kv_update_item(
   const ffmi_attn_work w = wdp->w;
   // channels: 0 q lo, 1 q hi, 2 k lo, 3 k hi, 4 v lo, 5 v hi
   f4 x[U][6], y[U][6], cs[U][2];  // y: second fp32 slab
-  constexpr int U4 = PSRC == 2 ? U : 1;
-  f4 z2[U4][6], z3[U4][6];  // PSRC 2: slabs 2 and 3
   int tslot[U], treq[U];  // (scalar fields: a struct copy would go to scratch)
   int tl[U], i0[U];
   // One round trip for every prologue load.  The RoPE positions of the
@@ -145,7 +142,7 @@ __device__ __forceinline__ void kv_update_item(
     const int col[6] = {h * D + i0[u], h * D + i0[u] + HD, Hl + h * D + i0[u],
                         Hl + h * D + i0[u] + HD, 2 * Hl + h * D + i0[u],
                         2 * Hl + h * D + i0[u] + HD};
-    if (PSRC >= 1 || (PSRC < 0 && part)) {  // slabs 0 and 1 (slab 0 again when pS == 1: no branch)
+    if (PSRC == 1 || (PSRC < 0 && part)) {  // slabs 0 and 1 (slab 0 again when pS == 1: no branch)
       const float *p1 = part + (pS > 1 ? (size_t)T * pNP : 0);
 #pragma unroll
       for (int c = 0; c < 6; ++c)
@@ -153,16 +150,6 @@ __device__ __forceinline__ void kv_update_item(
 #pragma unroll
       for (int c = 0; c < 6; ++c)
         y[u][c] = *reinterpret_cast<const f4 *>(p1 + (size_t)t * pNP + col[c]);
-      if constexpr (PSRC == 2) {  // slabs 2 and 3 (clamped to the last: no branch)
-        const float *p2 = part + (size_t)min(2, pS - 1) * T * pNP;
-        const float *p3 = part + (size_t)min(3, pS - 1) * T * pNP;
-#pragma unroll
-        for (int c = 0; c < 6; ++c)
-          z2[u][c] = *reinterpret_cast<const f4 *>(p2 + (size_t)t * pNP + col[c]);
-#pragma unroll
-        for (int c = 0; c < 6; ++c)
-          z3[u][c] = *reinterpret_cast<const f4 *>(p3 + (size_t)t * pNP + col[c]);
-      }
     } else {  // raw fp16 bits now, converted after every load is out
 #pragma unroll
       for (int c = 0; c < 6; ++c) {
@@ -202,23 +189,14 @@ __device__ __forceinline__ void kv_update_item(
         const uint32_t a = __float_as_uint(y[u][c][0]), b = __float_as_uint(y[u][c][1]);
         x[u][c] = f4{h2f(a & 0xffff), h2f(a >> 16), h2f(b & 0xffff), h2f(b >> 16)};
       }
-  if (PSRC >= 1 || (PSRC < 0 && part)) {  // slabs in slice order, then fp16 (partials_value)
+  if (PSRC == 1 || (PSRC < 0 && part)) {  // slabs in slice order, then fp16 (partials_value)
     if (pS > 1)
 #pragma unroll
       for (int u = 0; u < U; ++u)
 #pragma unroll
         for (int c = 0; c < 6; ++c) x[u][c] += y[u][c];
-    if constexpr (PSRC == 2) {
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-#pragma unroll
-        for (int c = 0; c < 6; ++c) {
-          if (pS > 2) x[u][c] += z2[u][c];
-          if (pS > 3) x[u][c] += z3[u][c];
-        }
-    }
     const size_t slab = (size_t)T * pNP;
-    for (int sl = PSRC == 2 ? 4 : 2; sl < pS; ++sl)
+    for (int sl = 2; sl < pS; ++sl)
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int t = w.q_start + (tl[u] < w.q_count ? tl[u] : 0);
@@ -885,9 +863,6 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
     if (!FU)                                                                                    \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, false>), grid, dim3(512), 0, s, blob, qbuf, \
                          kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                             \
-    else if (kv.part && kv.pS > 2)                                                              \
-      hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 2>), grid, dim3(512), 0, s,    \
-                         blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                 \
     else if (kv.part)                                                                           \
       hipLaunchKernelGGL((attention_kernel<D, QT, 8, true, false, 1>), grid, dim3(512), 0, s,    \
                          blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());                 \
@@ -915,10 +890,7 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
   }
   if (max_q > 16 && fused && attn_qsplit(W * heads)) {
     const dim3 grid2(W, heads, 2);
-    if (kv.part && kv.pS > 2)
-      hipLaunchKernelGGL((attention_kernel<D, 1, 8, true, false, 2, false, 2>), grid2, dim3(512), 0,
-                         s, blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
-    else if (kv.part)
+    if (kv.part)
       hipLaunchKernelGGL((attention_kernel<D, 1, 8, true, false, 1, false, 2>), grid2, dim3(512), 0,
                          s, blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
     else

@@ -878,117 +878,6 @@ __global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
   }
 }
 
-// ---------------------------------------------------------------------------
-// Wide M-split GEMM (verify batches of 129..192 rows): 8 waves, one
-// workgroup = all 12 m-tiles x NTW weight tiles x a K slice.
-//
-// Why: the M-split kernel above is bound by each CU's intake of requested
-// bytes (~45-50 GB/s per CU, L2 hits included), and every one
-// of its workgroups reads ALL of X for its NTW <= 8 tiles.  Here waves 0-3
-// load the X fragments and waves 4-7 the weight fragments of a k-step (each
-// byte requested ONCE per CU), both land in an LDS double buffer, and each
-// wave multiplies 3 m-tiles (row group w & 3) by NTW/2 tiles (column half
-// w >> 2) from LDS: twice the columns per X byte of the 4-wave kernel, so
-// with K split over S workgroups the per-CU intake per weight byte falls
-// (gate/up at T = 168: 2.1 MB per CU unsplit -> 1.5 MB at NTW 12, S 2).
-// Reduction order per output: MFMA chain over the slice's k-steps, slices
-// 0..S-1 summed by the consumer -- fixed by (N, K, S).
-// ---------------------------------------------------------------------------
-template <int NTW, int PF, int EPI, bool NTL>
-__global__ __launch_bounds__(512, 1) void gemm_wide_kernel(
-    const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp, uint16_t *__restrict__ Y,
-    float *__restrict__ Ypart, int T, int N, int KT, int NTILES, int S, int yp, size_t wts,
-    size_t wks) {
-  constexpr int MT = 12;         // m-tiles per workgroup (192 rows)
-  constexpr int XPW = MT / 4;    // X fragments per loader wave (waves 0-3)
-  constexpr int WPW = NTW / 4;   // weight fragments per loader wave (waves 4-7)
-  constexpr int FPW = XPW > WPW ? XPW : WPW;
-  constexpr int NTH = NTW / 2;   // tiles per computing wave (one column half)
-  static_assert(NTW % 4 == 0, "gate/up tile pairs inside each column half");
-  __shared__ __attribute__((aligned(16))) h8 sF[2][MT + NTW][64];
-  const int lane = threadIdx.x & 63;
-  const int wave = threadIdx.x >> 6;
-  const int rg = wave & 3, cg = wave >> 2;
-  const bool xw = wave < 4;  // wave-uniform role of the loads
-  const int tile0 = blockIdx.x * NTW;
-  const int ks = blockIdx.y;
-  const int per = (KT + S - 1) / S;
-  const int kb = min(KT, ks * per);
-  const int ke = min(KT, kb + per);
-  const int mlast = (T - 1) >> 4;
-  // this wave's load sources and LDS slots
-  const uint16_t *src[FPW];
-  int slot[FPW];
-#pragma unroll
-  for (int i = 0; i < FPW; ++i) {
-    if (xw) {
-      const int f = min(rg * XPW + i, MT - 1);
-      const int mt = min(f, mlast);
-      src[i] = X + ((size_t)mt * KT * 64 + lane) * 8;
-      slot[i] = f;
-    } else {
-      const int f = min(rg * WPW + i, NTW - 1);
-      src[i] = Wp + (size_t)min(tile0 + f, NTILES - 1) * wts + lane * 8;
-      slot[i] = MT + f;
-    }
-  }
-  auto ld = [&](h8 (&r)[FPW], int k) {
-    if (xw) {
-#pragma unroll
-      for (int i = 0; i < XPW; ++i) r[i] = *reinterpret_cast<const h8 *>(src[i] + (size_t)k * 512);
-    } else {
-#pragma unroll
-      for (int i = 0; i < WPW; ++i) r[i] = ld_weight<NTL>(src[i] + (size_t)k * wks);
-    }
-  };
-  auto st = [&](const h8 (&r)[FPW], int buf) {
-    if (xw) {
-#pragma unroll
-      for (int i = 0; i < XPW; ++i) sF[buf][slot[i]][lane] = r[i];
-    } else {
-#pragma unroll
-      for (int i = 0; i < WPW; ++i) sF[buf][slot[i]][lane] = r[i];
-    }
-  };
-  f4 acc[3][NTH];
-#pragma unroll
-  for (int i = 0; i < 3; ++i)
-#pragma unroll
-    for (int j = 0; j < NTH; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
-  if (kb < ke) {
-    h8 ring[PF][FPW];
-#pragma unroll
-    for (int q = 0; q < PF; ++q) ld(ring[q], min(kb + q, ke - 1));
-    st(ring[0], 0);
-    __syncthreads();
-    int cur = 0;
-    auto step = [&](auto Qc, int kt) {
-      constexpr int Q = decltype(Qc)::value;
-      h8 xa[3], wb[NTH];
-#pragma unroll
-      for (int i = 0; i < 3; ++i) xa[i] = sF[cur][rg * 3 + i][lane];
-#pragma unroll
-      for (int j = 0; j < NTH; ++j) wb[j] = sF[cur][MT + cg * NTH + j][lane];
-#pragma unroll
-      for (int i = 0; i < 3; ++i)
-#pragma unroll
-        for (int j = 0; j < NTH; ++j)  // D = W . X^T (mid_store's layout)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wb[j], xa[i], acc[i][j], 0, 0, 0);
-      ld(ring[Q], min(kt + PF, ke - 1));
-      st(ring[(Q + 1) % PF], cur ^ 1);  // k-step kt + 1
-      __syncthreads();
-      cur ^= 1;
-    };
-    int kt0 = kb;
-    for (; kt0 + PF <= ke; kt0 += PF)
-      static_for<PF>([&](auto Qc) { step(Qc, kt0 + decltype(Qc)::value); });
-    static_for<PF - 1>([&](auto Qc) {
-      if (kt0 + decltype(Qc)::value < ke) step(Qc, kt0 + decltype(Qc)::value);
-    });
-  }
-  mid_store<3, NTH, EPI>(acc, Y, Ypart, T, N, NTILES, S, ks, tile0 + cg * NTH, rg * 48, lane, yp);
-}
-
 static long long *stamp_buf() {
   static long long *buf = nullptr;
   if (!buf) {
@@ -1122,48 +1011,6 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   return p;
 }
 
-// Wide-kernel plan (gemm_wide_kernel) for one 129..192-row block: NTW tiles
-// and K slices per workgroup, or {0, 0} to keep the 4-wave kernel.
-// FFMI_WIDE: 0 off (default until measured), 1 on, and "NTW,S" or
-// "N:K:NTW,S;..." forces.
-struct WidePlan {
-  int NTW, S;
-};
-static WidePlan wide_plan(int T, int N, int K, int epi, int max_s = 8) {
-  WidePlan p{0, 0};
-  const int mtiles = (T + 15) / 16;
-  if (mtiles <= 8 || mtiles > 12) return p;
-  static const char *env = getenv("FFMI_WIDE");
-  if (!env || (env[0] == '0' && env[1] == 0)) return p;
-  const int KT = K / 32;
-  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
-  if (env && strchr(env, ',')) {
-    const char *q = env;
-    while (q && *q) {
-      int a = 0, b = 0, c = 0, d = 0;
-      const int n = sscanf(q, "%d:%d:%d,%d", &a, &b, &c, &d);
-      if (n == 4 && a == N && b == K) return WidePlan{c, d};
-      if (n != 4 && sscanf(q, "%d,%d", &a, &b) == 2) return WidePlan{a, b};
-      q = strchr(q, ';');
-      if (q) ++q;
-    }
-    return p;
-  }
-  // one wave of <= 256 workgroups, >= 8 k-steps per slice, 12 tiles where
-  // the grid allows
-  // (the residual norm combines <= 8 slabs at these widths)
-  // (NTW 8 reads the bytes per CU of the 4-wave kernel's NTW 8 plan: no gain)
-  for (int ntw : {12, 16}) {
-    const int nblk = (ntiles + ntw - 1) / ntw;
-    int S = std::max(1, 256 / nblk);
-    S = std::min(S, std::min(max_s, std::max(1, KT / 8)));
-    if (epi) S = std::min(S, 2);
-    if (nblk * S < 192) continue;
-    return WidePlan{ntw, S};
-  }
-  return p;
-}
-
 size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
   epilogue &= ~(FFMI_X_PACKED | FFMI_Y_PACKED | FFMI_W_STREAM);
   const int mtiles = (T + 15) / 16;
@@ -1172,10 +1019,8 @@ size_t gemm_workspace_bytes(int T, int N, int K, int epilogue) {
     return S > 1 ? (size_t)S * T * ((N + 15) / 16) * 16 * sizeof(float) : 0;
   }
   const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
-  const int S = std::max(std::max(mid_plan(T, N, K, epilogue, false).S,
-                                  epilogue ? 1 : mid_plan(T, N, K, epilogue, true).S),
-                         std::max(wide_plan(T, N, K, epilogue).S,
-                                  epilogue ? 1 : wide_plan(T, N, K, epilogue, 16).S));
+  const int S = std::max(mid_plan(T, N, K, epilogue, false).S,
+                         epilogue ? 1 : mid_plan(T, N, K, epilogue, true).S);
   return S > 1 ? (size_t)S * T * ntiles * 16 * sizeof(float) : 0;
 }
 
@@ -1252,52 +1097,6 @@ static hipError_t run_mid(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, fl
   return hipGetLastError();
 }
 
-template <int NTW>
-static hipError_t run_wide(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float *ws,
-                           size_t ws_bytes, int T, int N, int K, int epi, hipStream_t s, int yp,
-                           int S, Partials *defer, bool nt, int wpitch) {
-  const int KT = K / 32;
-  const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
-  const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch ? wpitch : ntiles);
-  const int nblk = (ntiles + NTW - 1) / NTW;
-  const size_t need = (size_t)S * T * ntiles * 16 * sizeof(float);
-  if (S > 1 && (!ws || ws_bytes < need)) return hipErrorInvalidValue;
-  dim3 grid(nblk, S);
-#define FFMI_WIDE_L(E, NL)                                                                    \
-  hipLaunchKernelGGL((gemm_wide_kernel<NTW, 4, E, NL>), grid, dim3(512), 0, s, X, Wp, Y, ws, T, \
-                     N, KT, ntiles, S, yp, wts, wks)
-  if (epi) {
-    if (nt) FFMI_WIDE_L(1, true);
-    else FFMI_WIDE_L(1, false);
-  } else {
-    if (nt) FFMI_WIDE_L(0, true);
-    else FFMI_WIDE_L(0, false);
-  }
-#undef FFMI_WIDE_L
-  if (defer) {
-    defer->S = 0;
-    if (S > 1 && !epi) {
-      defer->p = ws, defer->S = S, defer->NP = ntiles * 16;
-      return hipGetLastError();
-    }
-  }
-  if (S > 1) {
-    const long total = (long)T * ((N + 3) / 4);
-    const unsigned blocks = (unsigned)((total + 255) / 256);
-    if (epi) hipLaunchKernelGGL((gemm_reduce_kernel<1, 2>), dim3(blocks), dim3(256), 0, s, ws, Y, T,
-                                N, ntiles, S, yp);
-    else if (S <= 2) hipLaunchKernelGGL((gemm_reduce_kernel<0, 2>), dim3(blocks), dim3(256), 0, s,
-                                        ws, Y, T, N, ntiles, S, yp);
-    else if (S <= 4) hipLaunchKernelGGL((gemm_reduce_kernel<0, 4>), dim3(blocks), dim3(256), 0, s,
-                                        ws, Y, T, N, ntiles, S, yp);
-    else if (S <= 8) hipLaunchKernelGGL((gemm_reduce_kernel<0, 8>), dim3(blocks), dim3(256), 0, s,
-                                        ws, Y, T, N, ntiles, S, yp);
-    else hipLaunchKernelGGL((gemm_reduce_kernel<0, 16>), dim3(blocks), dim3(256), 0, s, ws, Y, T,
-                            N, ntiles, S, yp);
-  }
-  return hipGetLastError();
-}
-
 hipError_t launch_partials_reduce(const Partials &p, uint16_t *Y, int T, int N, hipStream_t s) {
   if (T <= 0 || p.S <= 0) return hipSuccess;
   // (> 8: the per-head o-projection slabs of a small model, OprojArgs)
@@ -1345,18 +1144,6 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
     if (fuse->kind == 1) FFMI_FZ(2, 1);
     FFMI_FZ(2, 2);
 #undef FFMI_FZ
-  }
-  if (mtiles > 8 && mtiles <= 12 && xp) {
-    const WidePlan w = wide_plan(T, N, K, epilogue, defer ? defer->max_s : 8);
-    if (w.NTW) {
-#define FFMI_WRUN(NW) \
-  return run_wide<NW>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, yp, w.S, defer, nt, wpitch)
-      if (w.NTW == 12) FFMI_WRUN(12);
-      if (w.NTW == 16) FFMI_WRUN(16);
-      if (w.NTW == 8) FFMI_WRUN(8);
-      if (w.NTW == 24) FFMI_WRUN(24);
-#undef FFMI_WRUN
-    }
   }
   if (mtiles > 4) {
     const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);

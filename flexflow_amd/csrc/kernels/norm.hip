@@ -165,14 +165,14 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   const float *pp = x2p.S > 0 ? x2p.p : nullptr;
   // > 8 slabs: the per-head o-projection slabs of a small model (OprojArgs,
   // <= 16 heads, H <= 1024)
-  if (pp && (x2p.S > 16 || (x2p.S > 8 && nchunk > 512))) return hipErrorInvalidValue;
+  if (pp && (x2p.S > 16 || (x2p.S > 8 && nchunk > 128))) return hipErrorInvalidValue;
   if ((x2 || pp) && !res_out) return hipErrorInvalidValue;
   // split-K slabs: one 8-column chunk per thread (H <= 8192); the model does
   // not defer its o/down partials beyond that
   if (pp && nchunk > 1024) return hipErrorInvalidValue;
   const int src = gather ? 3 : pp ? 2 : x2 ? 1 : 0;
   const int ms = !pp || x2p.S <= 1 ? 1 : x2p.S <= 2 ? 2 : x2p.S <= 4 ? 4 : x2p.S <= 8 ? 8
-               : x2p.S <= 12 && nchunk <= 128 ? 12 : 16;
+               : x2p.S <= 12 ? 12 : 16;
 #define FFMI_RMS3(NT, MC, MS, SR)                                                              \
   hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS, SR>), dim3(T), dim3(NT), 0, s, x1, x2, w,    \
                      res_out, out, H, eps, op, pp, x2p.S, x2p.NP, gather,               \
@@ -197,7 +197,6 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
   else if (nchunk <= 128 && ms == 16) FFMI_RMS3(128, 1, 16, 2);
   else if (nchunk <= 128) FFMI_RMS(128, 1);
   else if (nchunk <= 256) FFMI_RMS(256, 1);
-  else if (nchunk <= 512 && ms > 8) FFMI_RMS3(512, 1, 16, 2);  // wide-GEMM slabs (H <= 4096)
   else if (nchunk <= 512) FFMI_RMS(512, 1);
   else if (nchunk <= 1024) FFMI_RMS(1024, 1);
   else if (nchunk <= 2048) FFMI_RMS_NOSLAB(1024, 2);

@@ -805,7 +805,6 @@ struct LlamaGPU : public ffmi_model {
       }
       pr = prof_begin(on);
       ffmi::Partials qkv_part;
-      qkv_part.max_s = 4;  // the attention prologue loads <= 4 slabs in one round trip
       FFMI_HIP(ffmi::launch_gemm(fz_in ? res : h, L.wqkv, qkv, (float *)ws, ws_bytes, T, 3 * Hl, H,
                                  fz_in ? wstream : XP, stream, &qkv_part, 0,
                                  fz_in ? &fz_qkv : nullptr));
@@ -835,7 +834,6 @@ struct LlamaGPU : public ffmi_model {
         mk();
       } else if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
-        o_part.max_s = H <= 4096 ? 16 : 8;  // the residual norm combines the slabs
         FFMI_HIP(ffmi::launch_gemm(att, L.wo, proj, (float *)ws, ws_bytes, T, H, Hl, XP, stream,
                                    H <= 8192 ? &o_part : nullptr));
         prof_end(pr, GEMM_O, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
@@ -874,7 +872,6 @@ struct LlamaGPU : public ffmi_model {
         mk();
       } else if (o.tp_size == 1 || solo) {
         pr = prof_begin(on);
-        down_part.max_s = H <= 4096 ? 16 : 8;
         FFMI_HIP(ffmi::launch_gemm(mlp, L.wd, proj, (float *)ws, ws_bytes, T, H, Fl, XP, stream,
                                    H <= 8192 ? &down_part : nullptr));
         prof_end(pr, GEMM_DOWN, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
