@@ -493,7 +493,10 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&tmp, tmp_elems));
     // synthetic inits (ffmi_model_opts.weight_init; oracle orc_model_create_ex):
     // 1 scales o/down by 1/sqrt(2L); 2 (token chain) scales the embeddings by
-    // 128 and makes lm_head the permuted unscaled embedding rows
+    // 128, doubled while the layers' residual noise sqrt(L (H + 2F)) outgrows
+    // LLaMA-7B's by the same factor (oracle.h orc_chain_embed_scale: the
+    // chain's logit margin stays at least 7B's), and makes lm_head the
+    // permuted unscaled embedding rows
     FFMI_CHECK(o.weight_init >= 0 && o.weight_init <= 2, FFMI_ERR_INVALID);
     const int kres = o.weight_init == 1 ? (FFMI_WKIND_DEPTH | c.num_layers) : 0;
     auto fill = [&](uint16_t *dst, size_t n, const std::string &name, int kind, int cols = 0,
@@ -505,8 +508,13 @@ struct LlamaGPU : public ffmi_model {
       return FFMI_OK;
     };
     const bool chain = o.weight_init == 2 && weights_folder.empty();
+    float chain_scale = 128.0f;
+    for (long long f2 = 1; f2 * 32LL * (4096 + 2 * 11008) <
+                           (long long)c.num_layers * (c.hidden + 2LL * c.intermediate);
+         f2 *= 4)
+      chain_scale *= 2.0f;
     TRY(alloc(&embed, (size_t)V * H));
-    TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0, 0, 1, chain ? 128.0f : 1.0f));
+    TRY(fill(embed, (size_t)V * H, "model.embed_tokens.weight", 0, 0, 1, chain ? chain_scale : 1.0f));
     TRY(alloc(&final_norm, H));
     TRY(fill(final_norm, H, "model.norm.weight", 1));
     TRY(alloc(&lm, ffmi_linear_packed_bytes(Vl, H) / 2));

@@ -331,8 +331,9 @@ typedef struct {
   /* synthetic weights (no weights_folder), oracle.h orc_model_create_ex:
    * 0: every matrix uniform with std 0.02 (the bench's model);
    * 1: depth-scaled -- o_proj / down_proj at std 0.02 / sqrt(2L);
-   * 2: token chain -- embeddings x 128 and lm_head = the embedding rows
-   *    permuted (v -> (7919 v + 17) mod vocab): a peaked model whose greedy
+   * 2: token chain -- embeddings x 128 (x 2 per doubling of the residual
+   *    noise sqrt(L (H + 2F)) over LLaMA-7B's; 65B: x 512) and lm_head = the
+   *    embedding rows permuted (v -> (7919 v + 17) mod vocab): a peaked model whose greedy
    *    picks lead by margins far above fp16 rounding noise (parity tests of
    *    the reference's literal token bars; SpecInfer with full acceptance) */
   int weight_init;

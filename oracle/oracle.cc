@@ -632,6 +632,15 @@ extern "C" orc_model *orc_model_create(const orc_config *cfg, uint64_t seed,
   return orc_model_create_ex(cfg, seed, fp16, max_requests, max_seq, 0);
 }
 
+extern "C" float orc_chain_embed_scale(int num_layers, int hidden, int intermediate) {
+  const long long ref = 32LL * (4096 + 2 * 11008);  // LLaMA-7B
+  const long long own = (long long)num_layers * (hidden + 2LL * intermediate);
+  long long f2 = 1;  // (scale / 128)^2
+  float s = 128.0f;
+  while (f2 * ref < own) f2 *= 4, s *= 2.0f;
+  return s;
+}
+
 extern "C" orc_model *orc_model_create_ex(const orc_config *cfg, uint64_t seed, int fp16,
                                           int max_requests, int max_seq, int weight_init) {
   if (cfg->num_kv_heads != cfg->num_heads) return nullptr;  // MHA only
@@ -643,11 +652,12 @@ extern "C" orc_model *orc_model_create_ex(const orc_config *cfg, uint64_t seed, 
   m->d = cfg->hidden / cfg->num_heads;
   const size_t H = cfg->hidden, F = cfg->intermediate, Vv = cfg->vocab_size;
   if (weight_init == 2) {
-    // token-chain init: embeddings x ORC_CHAIN_EMBED_SCALE, lm_head row v =
+    // token-chain init: embeddings x orc_chain_embed_scale, lm_head row v =
     // the unscaled embedding row of perm(v) (a tied, permuted head): the
     // residual stream keeps the input token's direction, so the logit of
     // perm^-1(token) leads by a margin far above fp16 rounding noise
-    gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16, 0, 1, ORC_CHAIN_EMBED_SCALE);
+    gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16, 0, 1,
+        orc_chain_embed_scale(cfg->num_layers, cfg->hidden, cfg->intermediate));
     gen(m->lm, "model.embed_tokens.weight", seed, 0, Vv * H, fp16, (int)H, ORC_CHAIN_A);
   } else {
     gen(m->emb, "model.embed_tokens.weight", seed, 0, Vv * H, fp16);

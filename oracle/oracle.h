@@ -64,10 +64,15 @@ float orc_weight_amp(int kind);
  * amplitude times `scale` */
 void orc_gen_weight_rows(const char *name, uint64_t seed, int kind, size_t n, int cols,
                          uint64_t pa, uint64_t pb, float scale, float *out);
-/* token-chain init (weight_init 2): embedding scale and the lm_head row
- * permutation v -> (v * ORC_CHAIN_A + ORC_CHAIN_B) mod vocab (7919 is prime,
- * so a bijection for every vocabulary it does not divide) */
-#define ORC_CHAIN_EMBED_SCALE 128.0f
+/* token-chain init (weight_init 2): the lm_head row permutation
+ * v -> (v * ORC_CHAIN_A + ORC_CHAIN_B) mod vocab (7919 is prime, so a
+ * bijection for every vocabulary it does not divide) and the embedding scale:
+ * 128, doubled while the random layers' residual noise (grows like
+ * sqrt(L * (H + 2F))) outgrows LLaMA-7B's by the same factor -- the input
+ * token's share of the final residual, and so the chain's logit margin,
+ * stays at least 7B's (65B: 512).  Powers of two keep the fp16 scaling
+ * exact; the GPU init computes the same (llama_gpu.cpp) */
+float orc_chain_embed_scale(int num_layers, int hidden, int intermediate);
 #define ORC_CHAIN_A 7919u
 #define ORC_CHAIN_B 17u
 
@@ -128,7 +133,7 @@ orc_model *orc_model_create(const orc_config *cfg, uint64_t seed, int fp16,
 /* weight_init 0: every matrix at amp 0.02*sqrt(3) (the bench's model);
  * 1: depth-scaled -- o_proj / down_proj at 1/sqrt(2L) of that (a residual
  * stream that does not amplify per-layer rounding; ffmi_model_opts);
- * 2: token chain -- embeddings x ORC_CHAIN_EMBED_SCALE and lm_head = the
+ * 2: token chain -- embeddings x orc_chain_embed_scale() and lm_head = the
  * embedding rows permuted (ORC_CHAIN_A/B): a peaked model whose greedy picks
  * lead by margins far above fp16 rounding noise */
 orc_model *orc_model_create_ex(const orc_config *cfg, uint64_t seed, int fp16,

@@ -66,6 +66,8 @@ def lib():
                                           ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]
         L.orc_weight_amp.restype = ctypes.c_float
         L.orc_weight_amp.argtypes = [ctypes.c_int]
+        L.orc_chain_embed_scale.restype = ctypes.c_float
+        L.orc_chain_embed_scale.argtypes = [ctypes.c_int] * 3
         L.orc_model_destroy.argtypes = [ctypes.c_void_p]
         L.orc_model_forward.argtypes = [ctypes.c_void_p, ctypes.c_int, _i32p,
                                         ctypes.c_int, ctypes.c_int, _f32p]
@@ -103,6 +105,11 @@ REF16 = 2  # oracle.h ORC_REF16: the reference's half compute type in GEMMs / pr
 
 def set_ref_block(k):
     lib().orc_set_ref_block(k)
+
+
+def chain_embed_scale(num_layers, hidden, intermediate):
+    """token-chain init's embedding scale (oracle.h orc_chain_embed_scale)"""
+    return lib().orc_chain_embed_scale(num_layers, hidden, intermediate)
 
 
 def set_dot_variant(v):

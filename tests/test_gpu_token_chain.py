@@ -16,7 +16,7 @@ of the residual stream.  Random logits (std 1.28 over 32000 ids) put the top
 two within that noise in ~2% of positions, so the first-30-tokens bar of
 cpp_inference_tests.sh:104-129 cannot bind there (the oracle flips itself).
 
-Token chain (weight_init "token_chain", include/ffmi.h): embeddings x 128 and
+Token chain (weight_init "token_chain", include/ffmi.h): embeddings x 128 (7B) and
 lm_head = the embedding rows permuted (v -> (7919 v + 17) mod 32000).  The
 residual stream keeps the input token's direction through all 32 random
 layers, so the greedy pick is perm^-1(input token) and leads the runner-up by

@@ -160,3 +160,22 @@ def test_oracle_forward_multi_equals_per_request_forwards():
     ref = np.vstack([a.forward(r, blk, len(prompts[r])) for r, blk in enumerate(blocks)])
     got = b.forward_multi([0, 1, 2], [3, 1, 6], [len(p) for p in prompts], np.concatenate(blocks))
     assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
+
+
+def test_token_chain_init_scale_and_chain():
+    """weight_init 2 (token chain, oracle.h orc_chain_embed_scale): the
+    embedding scale keeps the chain's margin at depth and width -- 128 up to
+    LLaMA-7B's residual noise, doubled per doubling beyond (65B: 512) -- and a
+    small model's greedy pick at every position is perm^-1 of its input token,
+    perm(v) = (7919 v + 17) mod vocab."""
+    assert O.chain_embed_scale(2, 768, 3072) == 128.0  # LLaMA-68M
+    assert O.chain_embed_scale(32, 4096, 11008) == 128.0  # 7B
+    assert O.chain_embed_scale(80, 8192, 22016) == 512.0  # 65B
+    assert O.chain_embed_scale(33, 4096, 11008) == 256.0
+    cfg = dict(num_layers=2, vocab_size=500, num_heads=4, num_kv_heads=4, hidden=128,
+               intermediate=256, rms_eps=1e-6, rope_theta=10000.0)
+    m = O.Model(cfg, 3, fp16=1, max_requests=1, max_seq=64, weight_init=2)
+    toks = np.random.default_rng(1).integers(3, 500, size=40).astype(np.int32)
+    ids, _ = O.softmax_argmax(m.forward(0, toks, 0))
+    inv = {(7919 * v + 17) % 500: v for v in range(500)}
+    assert [inv[int(t)] for t in toks] == ids.tolist()
