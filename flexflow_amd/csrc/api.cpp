@@ -313,6 +313,12 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
 }
 
 namespace ffmi {
+void rope_table_host(float *tab, int max_pos, int d, const ffmi_attn_cfg *cfg) {
+  std::vector<float> t;
+  rope_table(t, max_pos, d, cfg);
+  memcpy(tab, t.data(), t.size() * sizeof(float));
+}
+
 // FFMI_FAULT_ROPE_POS (tests only): positions >= from_pos rotate as
 // position + 1; from_pos < 0 restores the true table
 ffmi_status attn_rope_fault(ffmi_attn *h, int from_pos) {

@@ -29,7 +29,10 @@ __device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
 // value i: element src(i) of the stream, src = i, or for a row-permuted
 // [rows][cols] tensor (cols > 0) element (perm(r), c), perm(r) = (r * pa + pb)
 // mod rows (the token-chain init's tied lm_head, oracle.h orc_gen_weight_rows)
-__global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, float center, float amp,
+// (OUT = float: the full-precision model's fp32 weights, the same values
+// before the fp16 rounding -- the oracle's fp32 mode)
+template <class OUT>
+__global__ void fill_weight_kernel(OUT *dst, size_t n, uint64_t key, float center, float amp,
                                    int cols, uint64_t pa, uint64_t pb) {
   const uint64_t rows = cols > 0 ? n / cols : 1;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
@@ -40,7 +43,8 @@ __global__ void fill_weight_kernel(uint16_t *dst, size_t n, uint64_t key, float 
     float u = (float)(x >> 40) * (1.0f / 16777216.0f);
     float t = __fsub_rn(__fmul_rn(2.0f, u), 1.0f);
     float w = __fadd_rn(center, __fmul_rn(t, amp));
-    dst[i] = __half_as_ushort(__float2half_rn(w));
+    if constexpr (sizeof(OUT) == 4) dst[i] = w;
+    else dst[i] = __half_as_ushort(__float2half_rn(w));
   }
 }
 
@@ -57,8 +61,18 @@ hipError_t launch_fill_weight(uint16_t *dst, size_t n, uint64_t key, int kind, h
   if (n == 0) return hipSuccess;
   size_t blocks = (n + 255) / 256;
   if (blocks > 65536) blocks = 65536;
-  hipLaunchKernelGGL(fill_weight_kernel, dim3((unsigned)blocks), dim3(256), 0, s, dst, n, key,
-                     kind == 1 ? 1.0f : 0.0f, weight_amp(kind) * scale, cols, pa, pb);
+  hipLaunchKernelGGL(fill_weight_kernel<uint16_t>, dim3((unsigned)blocks), dim3(256), 0, s, dst, n,
+                     key, kind == 1 ? 1.0f : 0.0f, weight_amp(kind) * scale, cols, pa, pb);
+  return hipGetLastError();
+}
+
+hipError_t launch_fill_weight_f32(float *dst, size_t n, uint64_t key, int kind, hipStream_t s,
+                                  int cols, uint64_t pa, uint64_t pb, float scale) {
+  if (n == 0) return hipSuccess;
+  size_t blocks = (n + 255) / 256;
+  if (blocks > 65536) blocks = 65536;
+  hipLaunchKernelGGL(fill_weight_kernel<float>, dim3((unsigned)blocks), dim3(256), 0, s, dst, n,
+                     key, kind == 1 ? 1.0f : 0.0f, weight_amp(kind) * scale, cols, pa, pb);
   return hipGetLastError();
 }
 

@@ -13,6 +13,7 @@ struct ffmi_rm {
 
 extern "C" ffmi_status ffmi_model_create(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
                                          ffmi_model **out) {
+  if (o && o->full_precision) return ffmi::create_llama_f32(cfg, o, out);
   return ffmi::create_llama_gpu(cfg, o, out);
 }
 

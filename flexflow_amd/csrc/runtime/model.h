@@ -83,6 +83,9 @@ struct ffmi_model {
 namespace ffmi {
 ffmi_status create_llama_gpu(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
                              ffmi_model **out);
+// full precision (--use-full-precision): runtime/llama_f32.cpp
+ffmi_status create_llama_f32(const ffmi_llama_config *cfg, const ffmi_model_opts *o,
+                             ffmi_model **out);
 ffmi_status create_hash_model(int vocab, int mode, int max_requests, int max_seq,
                               int max_tree, uint64_t salt, int disagree_pct,
                               ffmi_model **out);

@@ -89,7 +89,8 @@ class ModelOpts(ctypes.Structure):
     _fields_ = [("mode", c_int), ("tp_rank", c_int), ("tp_size", c_int), ("comm", c_void_p),
                 ("max_requests", c_int), ("max_tokens", c_int), ("max_seq_len", c_int),
                 ("max_tree_tokens", c_int), ("weight_seed", c_uint64), ("use_graphs", c_int),
-                ("weights_folder", ctypes.c_char_p), ("weight_init", c_int)]
+                ("weights_folder", ctypes.c_char_p), ("weight_init", c_int),
+                ("full_precision", c_int)]
 
 
 class RMConfig(ctypes.Structure):
@@ -134,6 +135,7 @@ SIGNATURES = {
     "ffmi_linear_pack_weight": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_linear_pack_gate_up": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_linear": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
+    "ffmi_linear_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
     "ffmi_linear_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "ffmi_linear_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                c_size_t, c_void_p]),

@@ -20,11 +20,13 @@ class Model:
     def __init__(self, config: dict, mode: str = "inc", *, max_requests=8, max_tokens=128,
                  max_seq_len=512, max_tree_tokens=23, weight_seed=20250117, tp_rank=0,
                  tp_size=1, comm=None, weights_folder: Optional[str] = None,
-                 weight_init: Union[int, str] = 0):
+                 weight_init: Union[int, str] = 0, full_precision: bool = False):
         """weights_folder: a checkpoint in the reference's per-tensor format
         (see checkpoint.convert_hf_model); None: seeded synthetic weights,
         `weight_init` "uniform" (0, the bench's), "depth_scaled" (1) or
-        "token_chain" (2) -- include/ffmi.h ffmi_model_opts."""
+        "token_chain" (2) -- include/ffmi.h ffmi_model_opts.  full_precision:
+        the reference's --use-full-precision (every tensor fp32,
+        runtime/llama_f32.cpp); default the fp16 model."""
         L = F.lib()
         self.config = dict(config)
         self.mode = mode
@@ -32,7 +34,7 @@ class Model:
         opts = F.ModelOpts(self.MODES[mode], tp_rank, tp_size, comm.handle if comm else None,
                            max_requests, max_tokens, max_seq_len, max_tree_tokens, weight_seed, 0,
                            weights_folder.encode() if weights_folder else None,
-                           F.WEIGHT_INITS.get(weight_init, weight_init))
+                           F.WEIGHT_INITS.get(weight_init, weight_init), int(full_precision))
         h = ctypes.c_void_p()
         F.check(L.ffmi_model_create(ctypes.byref(cfg), ctypes.byref(opts), ctypes.byref(h)),
                 "ffmi_model_create")

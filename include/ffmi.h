@@ -188,6 +188,13 @@ ffmi_status ffmi_linear_pack_gate_up(const void *Wg, const void *Wu, int out_dim
  * overlap (use ffmi_linear_ws for that). */
 ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
                         int out_dim, int in_dim, int epilogue, ffmi_stream stream);
+/* Linear on DT_FLOAT (linear_kernels.cu:450-582 with the full-precision
+ * model's fp32 tensors): Y[T][out] = X[T][in] . W[out][in]^T, row-major fp32,
+ * exact fp32 arithmetic (v_mfma_f32_16x16x4_f32: an fmaf chain per k range,
+ * the k ranges of a workgroup summed in a fixed order).  in_dim % 32 == 0,
+ * out_dim % 16 == 0. */
+ffmi_status ffmi_linear_f32(const float *X, const float *W, float *Y, int T, int out_dim,
+                            int in_dim, ffmi_stream stream);
 /* same with a caller-owned workspace of ffmi_linear_workspace_bytes() bytes */
 size_t ffmi_linear_workspace_bytes(int T, int out_dim, int in_dim, int epilogue);
 ffmi_status ffmi_linear_ws(const void *X, const void *W_packed, void *Y, int T,
@@ -337,6 +344,11 @@ typedef struct {
    *    picks lead by margins far above fp16 rounding noise (parity tests of
    *    the reference's literal token bars; SpecInfer with full acceptance) */
   int weight_init;
+  /* 1: full precision -- the reference's --use-full-precision
+   * (spec_infer.cc:102, incr_decoding.cc:77): weights, activations, KV cache
+   * and softmax in fp32 (runtime/llama_f32.cpp, kernels/f32.hip); lm_head
+   * replicated under TP.  0: the fp16 model (the measured path). */
+  int full_precision;
 } ffmi_model_opts;
 
 typedef struct ffmi_model ffmi_model;

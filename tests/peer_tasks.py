@@ -151,3 +151,29 @@ def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ss
     lg = m.debug_tensor("logits")
     m.close()
     return {"tokens": toks, "tf_logits": lg.astype(np.float16), "tf_seqs": seqs}
+
+
+def tp_generate_f32_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ssm_cfg):
+    """Full precision (--use-full-precision) TP shard per rank: incr decoding
+    or SpecInfer (SSM replicated, also fp32), tokens only"""
+    B = len(prompts)
+    mtb = 256
+    kw = dict(max_requests=B, max_seq_len=128, full_precision=True)
+    if spec:
+        m = fa.Model(cfg, "tree", max_tokens=mtb + 23 * B, weight_seed=seed, tp_rank=rank,
+                     tp_size=n, comm=comm, **kw)
+        ssm = fa.Model(ssm_cfg, "beam", max_tokens=mtb + 23 * B, max_tree_tokens=23,
+                       weight_seed=68, **kw)
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=128, spec_tree_width=(1, 1, 3))
+        rm.register_ssm_model(ssm)
+        res = fa.generate(rm, m, prompts, max_length=max_length, spec=True)
+        ssm.close()
+    else:
+        m = fa.Model(cfg, "inc", max_tokens=mtb, weight_seed=seed, tp_rank=rank, tp_size=n,
+                     comm=comm, **kw)
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=128)
+        res = fa.generate(rm, m, prompts, max_length=max_length)
+    m.close()
+    return {"tokens": [r.output_tokens for r in res], "llm_steps": rm.stats().llm_steps}

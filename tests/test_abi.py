@@ -51,6 +51,22 @@ def test_invalid_arguments_return_status_not_abort():
     L = F.lib()
     assert L.ffmi_linear(None, None, None, 1, 16, 32, 0, None) == 1
     assert L.ffmi_rmsnorm(None, None, None, 1, 8, 1e-6, None) == 1
+    # the full-precision linear: null operands, then an in_dim off the k-block
+    assert L.ffmi_linear_f32(None, None, None, 1, 16, 32, None) == 1
+    assert L.ffmi_linear_f32(None, None, None, 1, 16, 48, None) == 5
     cfg = F.AttnCfg(0, 2, 96, 1, 16, 0, 16, 0.1, 10000.0, 0)  # head_dim 96 unsupported
     h = ctypes.c_void_p()
     assert L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(h)) == 5
+
+
+def test_full_precision_model_opts_and_no_device():
+    """ffmi_model_opts.full_precision (the reference's --use-full-precision)
+    routes creation to the fp32 model, which fails with NO_DEVICE here (no
+    GPU) rather than falling back to anything on the host."""
+    L = F.lib()
+    cfg = F.LlamaConfig.from_dict(dict(num_layers=1, vocab_size=64, num_heads=2, num_kv_heads=2,
+                                       hidden=128, intermediate=256))
+    opts = F.ModelOpts(F.MODEL_INC, 0, 1, None, 1, 16, 64, 0, 1, 0, None, 0, 1)
+    assert opts.full_precision == 1
+    h = ctypes.c_void_p()
+    assert L.ffmi_model_create(ctypes.byref(cfg), ctypes.byref(opts), ctypes.byref(h)) == 6
