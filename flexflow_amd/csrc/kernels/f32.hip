@@ -125,15 +125,15 @@ __global__ __launch_bounds__(256) void f32_gemm_kernel(const float *__restrict__
 hipError_t launch_gemm_f32(const float *X, const float *W, float *Y, int T, int N, int K,
                            hipStream_t s) {
   if (T <= 0 || N <= 0) return hipSuccess;
-  if (K <= 0 || K % 32 || N % 16) return hipErrorInvalidValue;
+  if (K <= 0 || K % 32) return hipErrorInvalidValue;
   if (T <= 16) {
-    hipLaunchKernelGGL((f32_gemm_kernel<1, 1, 1, 1, 4>), dim3(N / 16, 1), dim3(256), 0, s, X, W,
+    hipLaunchKernelGGL((f32_gemm_kernel<1, 1, 1, 1, 4>), dim3((N + 15) / 16, 1), dim3(256), 0, s, X, W,
                        Y, T, N, K);
   } else if (T <= 32) {
-    hipLaunchKernelGGL((f32_gemm_kernel<2, 1, 1, 1, 4>), dim3(N / 16, 1), dim3(256), 0, s, X, W,
+    hipLaunchKernelGGL((f32_gemm_kernel<2, 1, 1, 1, 4>), dim3((N + 15) / 16, 1), dim3(256), 0, s, X, W,
                        Y, T, N, K);
   } else if (T <= 64) {
-    hipLaunchKernelGGL((f32_gemm_kernel<4, 1, 1, 1, 4>), dim3(N / 16, 1), dim3(256), 0, s, X, W,
+    hipLaunchKernelGGL((f32_gemm_kernel<4, 1, 1, 1, 4>), dim3((N + 15) / 16, 1), dim3(256), 0, s, X, W,
                        Y, T, N, K);
   } else {
     hipLaunchKernelGGL((f32_gemm_kernel<2, 2, 2, 2, 1>), dim3((N + 63) / 64, (T + 63) / 64),
@@ -460,7 +460,7 @@ hipError_t launch_softmax_topk_f32(const float *logits, int T, int V, int k, int
 extern "C" ffmi_status ffmi_linear_f32(const float *X, const float *W, float *Y, int T,
                                        int out_dim, int in_dim, ffmi_stream stream) {
   FFMI_CHECK(T >= 0 && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
-  FFMI_CHECK(in_dim % 32 == 0 && out_dim % 16 == 0, FFMI_ERR_UNSUPPORTED);
+  FFMI_CHECK(in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
   FFMI_CHECK(T == 0 || (X && W && Y), FFMI_ERR_INVALID);
   FFMI_HIP(ffmi::launch_gemm_f32(X, W, Y, T, out_dim, in_dim, (hipStream_t)stream));
   return FFMI_OK;

@@ -987,11 +987,6 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   if (prefill_plan && p.mblocks >= 4) {
     p.NTW = 8;
     p.S = K >= 8192 && KT >= 2 ? 2 : 1;
-    // a narrow shard's prefill grid (e.g. the TP = 8 qkv: 12 tile blocks x 6
-    // row blocks = 72 workgroups) splits K until it holds min_wg workgroups
-    static const int min_wg = getenv("FFMI_PREFILL_MINWG") ? atoi(getenv("FFMI_PREFILL_MINWG")) : 0;
-    const long wg = (long)((ntiles + 7) / 8) * p.mblocks;
-    while (p.S < 8 && p.S < KT && wg * p.S < min_wg) ++p.S;
   }
   // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split of
   // every M-split launch; "N:K:NTW,S;..." only of the listed shapes

@@ -152,8 +152,8 @@ struct LlamaF32 : public ffmi_model {
     heads_l = c.num_heads / P;
     Hl = heads_l * d;
     Fl = F / P;
-    // the fp32 GEMM's shape rules (K % 32, N % 16) for every projection
-    FFMI_CHECK(H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0 && V % 16 == 0, FFMI_ERR_UNSUPPORTED);
+    // the fp32 GEMM's shape rule (K % 32) for every projection
+    FFMI_CHECK(H % 32 == 0 && Hl % 32 == 0 && Fl % 32 == 0, FFMI_ERR_UNSUPPORTED);
     FFMI_CHECK(P == 1 || o.comm, FFMI_ERR_INVALID);
     Tm = (o.max_tokens + 15) & ~15;
     // an attached transport too small for a [Tm][H] fp32 all-reduce needs a

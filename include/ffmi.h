@@ -191,8 +191,7 @@ ffmi_status ffmi_linear(const void *X, const void *W_packed, void *Y, int T,
 /* Linear on DT_FLOAT (linear_kernels.cu:450-582 with the full-precision
  * model's fp32 tensors): Y[T][out] = X[T][in] . W[out][in]^T, row-major fp32,
  * exact fp32 arithmetic (v_mfma_f32_16x16x4_f32: an fmaf chain per k range,
- * the k ranges of a workgroup summed in a fixed order).  in_dim % 32 == 0,
- * out_dim % 16 == 0. */
+ * the k ranges of a workgroup summed in a fixed order).  in_dim % 32 == 0. */
 ffmi_status ffmi_linear_f32(const float *X, const float *W, float *Y, int T, int out_dim,
                             int in_dim, ffmi_stream stream);
 /* same with a caller-owned workspace of ffmi_linear_workspace_bytes() bytes */

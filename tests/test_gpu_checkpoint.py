@@ -97,3 +97,27 @@ def test_missing_or_truncated_file_fails_loudly(tmp_path):
     with pytest.raises(fa.ffmi.FFMIError, match="norm.weight"):
         fa.Model(CFG, "inc", max_requests=2, max_tokens=16, max_seq_len=64,
                  weights_folder=str(tmp_path))
+
+
+def test_full_precision_checkpoint_equals_synthetic(tmp_path):
+    """--use-full-precision loads the fp32 files as they are (file_loader.cc
+    with DT_FLOAT): the fp32 model from the folder gives the same tokens as
+    the seeded fp32 model (identical weights, identical arithmetic), and a GQA
+    folder equals its replicated MHA twin"""
+    st = seeded_state(CFG, SEED)
+    fa.convert_hf_model(st, str(tmp_path / "mha"), dtype=np.float32)
+    ps = prompts(5)
+    a = run(CFG, ps, weights_folder=str(tmp_path / "mha"), full_precision=True)
+    assert a == run(CFG, ps, weight_seed=SEED, full_precision=True)
+    d = CFG["hidden"] // CFG["num_heads"]
+    st_gqa = dict(st)
+    for l in range(CFG["num_layers"]):
+        for x in "kv":
+            n = f"model.layers.{l}.self_attn.{x}_proj.weight"
+            st_gqa[n] = st[n][:2 * d]
+            st[n] = np.concatenate([st[n][:d], st[n][:d], st[n][d:2 * d], st[n][d:2 * d]])
+    fa.convert_hf_model(st_gqa, str(tmp_path / "gqa"), dtype=np.float32)
+    fa.convert_hf_model(st, str(tmp_path / "rep"), dtype=np.float32)
+    assert run(dict(CFG, num_kv_heads=2), ps, weights_folder=str(tmp_path / "gqa"),
+               full_precision=True) == run(CFG, ps, weights_folder=str(tmp_path / "rep"),
+                                           full_precision=True)

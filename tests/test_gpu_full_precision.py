@@ -35,7 +35,7 @@ FP32_TIE = 1e-4  # oracle logit gap below which two fp32 runs may pick different
 
 
 @pytest.mark.parametrize("T,N,K", [(1, 16, 32), (5, 48, 96), (8, 4096, 4096), (24, 2304, 768),
-                                   (33, 272, 1376), (64, 64, 3072), (168, 1536, 4096),
+                                   (33, 272, 1376), (64, 1000, 3072), (3, 40, 64), (168, 1536, 4096),
                                    (577, 96, 1376), (1024, 512, 4096)])
 def test_linear_f32_against_fp64(T, N, K):
     """ffmi_linear_f32 against an fp64 product: every element within the fp32
