@@ -289,11 +289,22 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   h->slots = (cfg->max_seq_len + cfg->max_tree_tokens + 31) & ~31;
   const size_t Hl = (size_t)cfg->num_heads * cfg->head_dim;
   const size_t kv = (size_t)cfg->max_requests * cfg->num_heads * h->slots * cfg->head_dim;
-  bool ok = hipMalloc((void **)&h->kc, kv * 2) == hipSuccess &&
-            hipMalloc((void **)&h->vc, kv * 2) == hipSuccess &&
-            hipMalloc((void **)&h->qbuf, (size_t)cfg->max_tokens * Hl * 2) == hipSuccess;
+  // element size: fp16, or fp32 for DT_FLOAT (the fp32 kernels stage one
+  // TREE batch: their commits run before the step's stores, no ping-pong)
+  const bool f32 = cfg->full_precision != 0;
+  if (f32 && (cfg->out_layout != 0 || (size_t)(cfg->head_dim + 256 + h->slots) * 4 > 64 * 1024)) {
+    delete h;
+    ffmi_set_last_error("full precision: out_layout 0 and (head_dim + 256 + slots) * 4 <= 64 KiB",
+                        __FILE__, __LINE__);
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  const size_t es = f32 ? 4 : 2, stage_halves = f32 ? 1 : 2;
+  bool ok = hipMalloc((void **)&h->kc, kv * es) == hipSuccess &&
+            hipMalloc((void **)&h->vc, kv * es) == hipSuccess &&
+            hipMalloc((void **)&h->qbuf, (size_t)cfg->max_tokens * Hl * es) == hipSuccess;
   if (ok && cfg->mode == FFMI_ATTN_TREE)
-    ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * 2 * 2) == hipSuccess;
+    ok = hipMalloc((void **)&h->stage, (size_t)cfg->max_tokens * 2 * Hl * es * stage_halves) ==
+         hipSuccess;
   std::vector<float> tab;
   rope_table(tab, h->slots, cfg->head_dim, cfg);
   if (ok) ok = hipMalloc((void **)&h->rope, tab.size() * sizeof(float)) == hipSuccess;
@@ -304,21 +315,16 @@ extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **ou
   }
   // zero the caches: masked keys are multiplied by exactly-zero weights, so
   // never-written slots must hold finite values
-  FFMI_HIP(hipMemset(h->kc, 0, kv * 2));
-  FFMI_HIP(hipMemset(h->vc, 0, kv * 2));
-  if (h->stage) FFMI_HIP(hipMemset(h->stage, 0, (size_t)cfg->max_tokens * 2 * Hl * 2 * 2));
+  FFMI_HIP(hipMemset(h->kc, 0, kv * es));
+  FFMI_HIP(hipMemset(h->vc, 0, kv * es));
+  if (h->stage)
+    FFMI_HIP(hipMemset(h->stage, 0, (size_t)cfg->max_tokens * 2 * Hl * es * stage_halves));
   FFMI_HIP(hipMemcpy(h->rope, tab.data(), tab.size() * sizeof(float), hipMemcpyHostToDevice));
   *out = h;
   return FFMI_OK;
 }
 
 namespace ffmi {
-void rope_table_host(float *tab, int max_pos, int d, const ffmi_attn_cfg *cfg) {
-  std::vector<float> t;
-  rope_table(t, max_pos, d, cfg);
-  memcpy(tab, t.data(), t.size() * sizeof(float));
-}
-
 // FFMI_FAULT_ROPE_POS (tests only): positions >= from_pos rotate as
 // position + 1; from_pos < 0 restores the true table
 ffmi_status attn_rope_fault(ffmi_attn *h, int from_pos) {
@@ -362,6 +368,19 @@ ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
   const bool tree = h->cfg.mode == FFMI_ATTN_TREE;
   const hipStream_t s = (hipStream_t)stream;
   const int heads = h->cfg.num_heads, d = h->cfg.head_dim;
+  if (h->cfg.full_precision) {
+    // DT_FLOAT: commits (TREE), then RoPE + KV store (+ staging), then the
+    // attention, each its own launch (kernels/f32.hip)
+    FFMI_CHECK(qkv && qkvp.S == 0 && !(opa && opa->wo), FFMI_ERR_INVALID);
+    FFMI_HIP(ffmi::launch_kv_update_f32(b->dev, b->num_tokens, tree ? b->num_commits : 0,
+                                        (const float *)qkv, h->rope, h->slots, (float *)h->qbuf,
+                                        (float *)h->kc, (float *)h->vc,
+                                        tree ? (float *)h->stage : nullptr, heads, d, h->slots, s));
+    FFMI_HIP(ffmi::launch_attention_f32(b->dev, b->num_tokens, (const float *)h->qbuf,
+                                        (const float *)h->kc, (const float *)h->vc, (float *)out,
+                                        heads, d, h->slots, h->cfg.qk_scale, s));
+    return FFMI_OK;
+  }
   uint16_t *stage_wr = nullptr, *stage_rd = nullptr;
   int C = 0;
   if (tree) {

@@ -132,15 +132,14 @@ hipError_t launch_fill_weight_f32(float *dst, size_t n, uint64_t key, int kind, 
                                   int cols = 0, uint64_t pa = 1, uint64_t pb = 0,
                                   float scale = 1.0f);
 float weight_amp(int kind);
-// RoPE cos/sin table [max_pos][d/2][2] of an attention config (api.cpp)
-void rope_table_host(float *tab, int max_pos, int d, const ffmi_attn_cfg *cfg);
 // ---- full-precision path (kernels/f32.hip) ----
 hipError_t launch_gemm_f32(const float *X, const float *W, float *Y, int T, int N, int K,
                            hipStream_t s);
 hipError_t launch_rmsnorm_f32(const float *x1, const float *x2, const float *w, float *res_out,
                               float *out, int T, int H, float eps, hipStream_t s,
                               const char *gather = nullptr);
-hipError_t launch_silu_mul_f32(const float *gu, float *out, int T, int F, hipStream_t s);
+hipError_t launch_silu_mul_f32(const float *A, const float *B, float *out, int T, int F,
+                               size_t lda, size_t ldb, hipStream_t s);
 hipError_t launch_kv_update_f32(const char *blob, int T, int C, const float *qkv, const float *rope,
                                 int max_rope_pos, float *qbuf, float *kc, float *vc,
                                 float *stage, int heads, int d, int slots, hipStream_t s);

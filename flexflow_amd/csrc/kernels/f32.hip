@@ -182,7 +182,9 @@ __global__ __launch_bounds__(256) void f32_rmsnorm_kernel(
   }
   ss = block_reduce256(ss, sh, [](double p, double q) { return p + q; });
   const float sum = (float)ss;
-  const float rms = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
+  // sqrtf: the correctly rounded square root (HIP's __fsqrt_rn is the native
+  // v_sqrt_f32, ~1 ulp, unless OCML_BASIC_ROUNDED_OPERATIONS is defined)
+  const float rms = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
   // (res_out may alias x1: read back this thread's own sums, never x1 + x2 again)
   for (int j = threadIdx.x; j < H; j += blockDim.x) {
     const float v = res_out ? res_out[(size_t)row * H + j] : (b ? __fadd_rn(a[j], b[j]) : a[j]);
@@ -199,25 +201,29 @@ hipError_t launch_rmsnorm_f32(const float *x1, const float *x2, const float *w, 
   return hipGetLastError();
 }
 
-// SigmoidSiluMulti (sigmoid_silu_multi.cu:37-47) on fp32: gu [T][2F] holds
-// gate in columns [0, F) and up in [F, 2F); out = (a * sigmoid(a)) * b
-__global__ void f32_silu_mul_kernel(const float *__restrict__ gu, float *__restrict__ out, int T,
-                                    int F) {
+// SigmoidSiluMulti (sigmoid_silu_multi.cu:37-47) on fp32: out[t][f] =
+// (a * sigmoid(a)) * b with a = A[t*lda + f], b = B[t*ldb + f] (the model's
+// [T][2F] gate|up product: B = A + F, lda = ldb = 2F)
+__global__ void f32_silu_mul_kernel(const float *__restrict__ A, const float *__restrict__ B,
+                                    float *__restrict__ out, int T, int F, size_t lda,
+                                    size_t ldb) {
   const size_t n = (size_t)T * F;
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n;
        i += (size_t)gridDim.x * blockDim.x) {
     const size_t t = i / F, f = i % F;
-    const float a = gu[t * 2 * F + f], b = gu[t * 2 * F + F + f];
+    const float a = A[t * lda + f], b = B[t * ldb + f];
     const float sg = __fdiv_rn(1.0f, __fadd_rn(1.0f, expf(-a)));
     out[i] = __fmul_rn(__fmul_rn(a, sg), b);
   }
 }
 
-hipError_t launch_silu_mul_f32(const float *gu, float *out, int T, int F, hipStream_t s) {
-  if (T <= 0) return hipSuccess;
+hipError_t launch_silu_mul_f32(const float *A, const float *B, float *out, int T, int F,
+                               size_t lda, size_t ldb, hipStream_t s) {
+  if (T <= 0 || F <= 0) return hipSuccess;
   const size_t n = (size_t)T * F;
   const unsigned blocks = (unsigned)std::min<size_t>((n + 255) / 256, 65536);
-  hipLaunchKernelGGL(f32_silu_mul_kernel, dim3(blocks), dim3(256), 0, s, gu, out, T, F);
+  hipLaunchKernelGGL(f32_silu_mul_kernel, dim3(blocks), dim3(256), 0, s, A, B, out, T, F, lda,
+                     ldb);
   return hipGetLastError();
 }
 
@@ -456,12 +462,42 @@ hipError_t launch_softmax_topk_f32(const float *logits, int T, int V, int k, int
 
 }  // namespace ffmi
 
-// public kernel-level entry (include/ffmi.h)
+// public kernel-level entries (include/ffmi.h)
 extern "C" ffmi_status ffmi_linear_f32(const float *X, const float *W, float *Y, int T,
                                        int out_dim, int in_dim, ffmi_stream stream) {
   FFMI_CHECK(T >= 0 && out_dim > 0 && in_dim > 0, FFMI_ERR_INVALID);
   FFMI_CHECK(in_dim % 32 == 0, FFMI_ERR_UNSUPPORTED);
   FFMI_CHECK(T == 0 || (X && W && Y), FFMI_ERR_INVALID);
   FFMI_HIP(ffmi::launch_gemm_f32(X, W, Y, T, out_dim, in_dim, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rmsnorm_f32(const float *x, const float *w, float *out, int T, int H,
+                                        float eps, ffmi_stream stream) {
+  FFMI_CHECK(x && w && out && T >= 0 && H > 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_rmsnorm_f32(x, nullptr, w, nullptr, out, T, H, eps, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_residual_rmsnorm_f32(const float *x1, const float *x2, const float *w,
+                                                 float *residual_out, float *out, int T, int H,
+                                                 float eps, ffmi_stream stream) {
+  FFMI_CHECK(x1 && x2 && w && residual_out && out && T >= 0 && H > 0, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_rmsnorm_f32(x1, x2, w, residual_out, out, T, H, eps, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_silu_mul_f32(const float *a, const float *b, float *out, size_t n,
+                                         ffmi_stream stream) {
+  FFMI_CHECK(a && b && out && n <= (size_t)INT32_MAX, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_silu_mul_f32(a, b, out, 1, (int)n, n, n, (hipStream_t)stream));
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_arg_topk_f32(const float *logits, int T, int V, int k, int32_t *ids,
+                                         float *probs, ffmi_stream stream) {
+  FFMI_CHECK(logits && ids && probs && T >= 0 && V > 0 && k >= 1 && k <= 4 && k <= V,
+             FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_softmax_topk_f32(logits, T, V, k, ids, probs, (hipStream_t)stream));
   return FFMI_OK;
 }

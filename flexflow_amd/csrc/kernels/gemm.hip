@@ -153,7 +153,7 @@ __global__ __launch_bounds__(KW * 64) void gemm_skinny_kernel(
         v += row_ror_f<8>(v);
         v = ((lane_f(v, 0) + lane_f(v, 16)) + lane_f(v, 32)) + lane_f(v, 48);
         if (lane == 0 && m < T) {
-          const float rf = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(v, (float)K), fz.eps)));
+          const float rf = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(v, (float)K), fz.eps)));
           sRms[m] = __half2float(__float2half_rn(rf));
         }
       }

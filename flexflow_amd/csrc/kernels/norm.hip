@@ -126,7 +126,9 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     }
   }
   const float sum = block_sum<NT / 64>(ss, scratch);
-  const float rms_f = __fdiv_rn(1.0f, __fsqrt_rn(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
+  // sqrtf: the correctly rounded square root (HIP's __fsqrt_rn is the native
+  // v_sqrt_f32, ~1 ulp, unless OCML_BASIC_ROUNDED_OPERATIONS is defined)
+  const float rms_f = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));
   const float rms = h2f_(f2h_(rms_f));
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {

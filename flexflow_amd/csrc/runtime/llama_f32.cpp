@@ -30,8 +30,7 @@ namespace {
 struct LayerF {
   float *in_norm = nullptr, *post_norm = nullptr;
   float *wqkv = nullptr, *wo = nullptr, *wgu = nullptr, *wd = nullptr;  // row-major [N][K]
-  float *kc = nullptr, *vc = nullptr;  // [req][head][slot][d]
-  float *stage = nullptr;  // TREE: this layer's rotated k / v of the last step's tokens
+  ffmi_attn *attn = nullptr;  // DT_FLOAT handle: fp32 KV cache, TREE staging, RoPE table
 };
 
 struct LlamaF32 : public ffmi_model {
@@ -41,9 +40,8 @@ struct LlamaF32 : public ffmi_model {
   int H = 0, F = 0, V = 0, d = 0, heads_l = 0, Hl = 0, Fl = 0, P = 1, slots = 0, Tm = 0;
   hipStream_t stream = nullptr;
   std::vector<LayerF> layers;
-  float *embed = nullptr, *final_norm = nullptr, *lm = nullptr, *rope = nullptr;
-  int rope_rows = 0;
-  float *res = nullptr, *h = nullptr, *qkv = nullptr, *qbuf = nullptr, *att = nullptr,
+  float *embed = nullptr, *final_norm = nullptr, *lm = nullptr;
+  float *res = nullptr, *h = nullptr, *qkv = nullptr, *att = nullptr,
         *proj = nullptr, *gu = nullptr, *mlp = nullptr, *logits = nullptr;
   int32_t *res_d = nullptr;  // [ids (T*k) | probs (T*k)] of a step
   int32_t *res_h = nullptr;  // pinned copy
@@ -57,6 +55,7 @@ struct LlamaF32 : public ffmi_model {
   ~LlamaF32() override {
     if (stream) (void)hipStreamSynchronize(stream);
     for (auto &kv : graphs) (void)hipGraphExecDestroy(kv.second);
+    for (auto &L : layers) ffmi_attn_destroy(L.attn);
     for (void *p : allocs) (void)hipFree(p);
     if (res_h) (void)hipHostFree(res_h);
     ffmi_batch_destroy(batch);
@@ -176,7 +175,6 @@ struct LlamaF32 : public ffmi_model {
     TRY(alloc(&res, (size_t)Tm * H));
     TRY(alloc(&h, (size_t)Tm * H));
     TRY(alloc(&qkv, (size_t)Tm * 3 * Hl));
-    TRY(alloc(&qbuf, (size_t)Tm * Hl));
     TRY(alloc(&att, (size_t)Tm * Hl));
     TRY(alloc(&proj, (size_t)Tm * H));
     TRY(alloc(&gu, (size_t)Tm * 2 * Fl));
@@ -185,21 +183,6 @@ struct LlamaF32 : public ffmi_model {
     TRY(alloc(&res_d, (size_t)Tm * 4 * 2));
     FFMI_HIP(hipHostMalloc((void **)&res_h, (size_t)Tm * 4 * 2 * sizeof(int32_t),
                            hipHostMallocDefault));
-    {  // RoPE table (the attention handle's, api.cpp rope_table)
-      ffmi_attn_cfg ac{};
-      ac.head_dim = d;
-      ac.rope_theta = c.rope_theta;
-      ac.rope_llama3 = c.rope_llama3;
-      ac.rope_factor = c.rope_factor;
-      ac.rope_low_freq_factor = c.rope_low_freq_factor;
-      ac.rope_high_freq_factor = c.rope_high_freq_factor;
-      ac.rope_original_max_pos = c.rope_original_max_pos;
-      rope_rows = slots;
-      std::vector<float> tab((size_t)slots * d);
-      rope_table_host(tab.data(), slots, d, &ac);
-      TRY(alloc(&rope, tab.size()));
-      FFMI_HIP(hipMemcpy(rope, tab.data(), tab.size() * 4, hipMemcpyHostToDevice));
-    }
     // weights: full tensors through a staging buffer, this shard's rows /
     // columns copied out
     float *tmp = nullptr;
@@ -223,7 +206,6 @@ struct LlamaF32 : public ffmi_model {
       TRY(full_tensor(lm, V, H, "lm_head.weight", 0));
     const int s = o.tp_rank;
     layers.resize(c.num_layers);
-    const size_t kv = (size_t)o.max_requests * heads_l * slots * d;
     for (int l = 0; l < c.num_layers; ++l) {
       LayerF &L = layers[l];
       const std::string p = "model.layers." + std::to_string(l) + ".";
@@ -253,16 +235,25 @@ struct LlamaF32 : public ffmi_model {
       TRY(alloc(&L.wd, (size_t)H * Fl));
       TRY(full_tensor(tmp, H, F, p + "mlp.down_proj.weight", kres));
       TRY(take(L.wd, tmp, F, 0, H, s * Fl, Fl));
-      // zeroed caches: never-written slots hold finite values
-      TRY(alloc(&L.kc, kv));
-      TRY(alloc(&L.vc, kv));
-      FFMI_HIP(hipMemsetAsync(L.kc, 0, kv * 4, stream));
-      FFMI_HIP(hipMemsetAsync(L.vc, 0, kv * 4, stream));
-      // per layer: the next step's commits read what THIS layer staged
-      if (mode == FFMI_MODEL_TREE) {
-        TRY(alloc(&L.stage, (size_t)Tm * 2 * Hl));
-        FFMI_HIP(hipMemsetAsync(L.stage, 0, (size_t)Tm * 2 * Hl * 4, stream));
-      }
+      // the layer's DT_FLOAT attention handle (ffmi_attn_cfg.full_precision)
+      ffmi_attn_cfg ac{};
+      ac.mode = mode == FFMI_MODEL_TREE ? FFMI_ATTN_TREE
+                                        : (mode == FFMI_MODEL_BEAM ? FFMI_ATTN_SPEC : FFMI_ATTN_INC);
+      ac.num_heads = heads_l;
+      ac.head_dim = d;
+      ac.max_requests = o.max_requests;
+      ac.max_seq_len = o.max_seq_len;
+      ac.max_tree_tokens = tree;
+      ac.max_tokens = Tm;
+      ac.qk_scale = 1.0f / sqrtf((float)d);
+      ac.rope_theta = c.rope_theta;
+      ac.rope_llama3 = c.rope_llama3;
+      ac.rope_factor = c.rope_factor;
+      ac.rope_low_freq_factor = c.rope_low_freq_factor;
+      ac.rope_high_freq_factor = c.rope_high_freq_factor;
+      ac.rope_original_max_pos = c.rope_original_max_pos;
+      ac.full_precision = 1;
+      TRY(ffmi_attn_create(&ac, &L.attn));
     }
     FFMI_HIP(hipStreamSynchronize(stream));
     for (auto it = allocs.begin(); it != allocs.end(); ++it)
@@ -283,9 +274,7 @@ struct LlamaF32 : public ffmi_model {
   // everything a step puts on the stream (llama.cc:55-295 on DT_FLOAT)
   ffmi_status enqueue(int k, size_t blob_bytes, bool record_upload) {
     const int T = (int)ps.tokens.size();
-    const int C = (int)ps.commits.size();
     const float eps = c.rms_eps;
-    const float scale = 1.0f / sqrtf((float)d);
     ffmi_status st;
 #define TRY(x) \
   do { if ((st = (x)) != FFMI_OK) return st; } while (0)
@@ -300,15 +289,12 @@ struct LlamaF32 : public ffmi_model {
       else
         FFMI_HIP(launch_rmsnorm_f32(res, proj, L.in_norm, res, h, T, H, eps, stream));
       FFMI_HIP(launch_gemm_f32(h, L.wqkv, qkv, T, 3 * Hl, H, stream));
-      FFMI_HIP(launch_kv_update_f32(blob, T, C, qkv, rope, rope_rows, qbuf, L.kc, L.vc, L.stage,
-                                    heads_l, d, slots, stream));
-      FFMI_HIP(launch_attention_f32(blob, T, qbuf, L.kc, L.vc, att, heads_l, d, slots, scale,
-                                    stream));
+      TRY(attn_forward(L.attn, batch, qkv, Partials(), att, (ffmi_stream)stream));
       FFMI_HIP(launch_gemm_f32(att, L.wo, proj, T, H, Hl, stream));
       TRY(allreduce(proj, (size_t)T * H));
       FFMI_HIP(launch_rmsnorm_f32(res, proj, L.post_norm, res, h, T, H, eps, stream));
       FFMI_HIP(launch_gemm_f32(h, L.wgu, gu, T, 2 * Fl, H, stream));
-      FFMI_HIP(launch_silu_mul_f32(gu, mlp, T, Fl, stream));
+      FFMI_HIP(launch_silu_mul_f32(gu, gu + Fl, mlp, T, Fl, 2 * (size_t)Fl, 2 * (size_t)Fl, stream));
       FFMI_HIP(launch_gemm_f32(mlp, L.wd, proj, T, H, Fl, stream));
       TRY(allreduce(proj, (size_t)T * H));
     }

@@ -562,7 +562,7 @@ struct LlamaGPU : public ffmi_model {
       TRY(alloc(&L.wd, ffmi_linear_packed_bytes(H, Fl) / 2));
       TRY(fill(tmp, (size_t)H * F, p + "mlp.down_proj.weight", kres));
       FFMI_HIP(launch_pack_weight(tmp, F, 0, s * Fl, H, Fl, L.wd, 1, 0, H / 16, stream));
-      ffmi_attn_cfg ac;
+      ffmi_attn_cfg ac{};  // (zeroed: fields added to the ABI later default to 0)
       ac.mode = mode == FFMI_MODEL_TREE ? FFMI_ATTN_TREE
                                         : (mode == FFMI_MODEL_BEAM ? FFMI_ATTN_SPEC : FFMI_ATTN_INC);
       ac.num_heads = heads_l;

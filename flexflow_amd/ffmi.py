@@ -65,7 +65,7 @@ class AttnCfg(ctypes.Structure):
                 ("max_tokens", c_int), ("qk_scale", c_float), ("rope_theta", c_float),
                 ("out_layout", c_int), ("rope_llama3", c_int), ("rope_factor", c_float),
                 ("rope_low_freq_factor", c_float), ("rope_high_freq_factor", c_float),
-                ("rope_original_max_pos", c_int)]
+                ("rope_original_max_pos", c_int), ("full_precision", c_int)]
 
 
 class LlamaConfig(ctypes.Structure):
@@ -136,6 +136,11 @@ SIGNATURES = {
     "ffmi_linear_pack_gate_up": (c_int, [c_void_p, c_void_p, c_int, c_int, c_void_p, c_void_p]),
     "ffmi_linear": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p]),
     "ffmi_linear_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_void_p]),
+    "ffmi_rmsnorm_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "ffmi_residual_rmsnorm_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int,
+                                          c_int, c_float, c_void_p]),
+    "ffmi_silu_mul_f32": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ffmi_arg_topk_f32": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ffmi_linear_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int]),
     "ffmi_linear_ws": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                c_size_t, c_void_p]),

@@ -126,6 +126,10 @@ typedef struct {
   int rope_llama3;
   float rope_factor, rope_low_freq_factor, rope_high_freq_factor;
   int rope_original_max_pos;
+  /* 1: DT_FLOAT (--use-full-precision): qkv in and out fp32 row-major
+   * (out_layout 0), K and V caches fp32 [req][head][slot][d] both, fp32
+   * softmax (kernels/f32.hip).  0: fp16. */
+  int full_precision;
 } ffmi_attn_cfg;
 
 typedef struct ffmi_attn ffmi_attn;
@@ -144,7 +148,8 @@ ffmi_status ffmi_attn_spec(ffmi_attn *h, const ffmi_batch_dev *b, const void *qk
 ffmi_status ffmi_attn_tree(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv,
                            void *out, ffmi_stream stream);
 /* test hooks: raw KV cache pointers and layout ([req][head][slot][d] for K,
- * [req][head][d][slot] for V, slots = max_seq_len + max_tree_tokens) */
+ * [req][head][d][slot] for V -- full precision: [req][head][slot][d] for
+ * both, fp32 -- slots = max_seq_len + max_tree_tokens rounded up to 32) */
 ffmi_status ffmi_attn_kv_ptrs(ffmi_attn *h, void **k, void **v, int *slots);
 
 /* ------------------------------------------------------------------------ */
@@ -285,6 +290,19 @@ ffmi_status ffmi_argmax(const void *logits, int T, int V, int32_t *ids,
 /* softmax + ArgTopK (arg_topk.cu:339-448), k <= 4, sorted, lower index on ties */
 ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, int32_t *ids,
                           float *probs, ffmi_stream stream);
+/* DT_FLOAT twins (--use-full-precision, kernels/f32.hip): RMSNorm /
+ * ResidualRMSNorm (sum of squares in fp64, rounded once; fp32 residual add),
+ * SigmoidSiluMulti, softmax + arg-top-k on fp32 probabilities (k <= 4, lowest
+ * index among equal probabilities; k = 1 is the argmax) */
+ffmi_status ffmi_rmsnorm_f32(const float *x, const float *w, float *out, int T, int H, float eps,
+                             ffmi_stream stream);
+ffmi_status ffmi_residual_rmsnorm_f32(const float *x1, const float *x2, const float *w,
+                                      float *residual_out, float *out, int T, int H, float eps,
+                                      ffmi_stream stream);
+ffmi_status ffmi_silu_mul_f32(const float *a, const float *b, float *out, size_t n,
+                              ffmi_stream stream);
+ffmi_status ffmi_arg_topk_f32(const float *logits, int T, int V, int k, int32_t *ids,
+                              float *probs, ffmi_stream stream);
 /* seeded synthetic weights, identical to oracle/orc_gen_weight then fp16.
  * kind 0: matrix (uniform, std 0.02); 1: norm weight (1 +- 0.1);
  * FFMI_WKIND_DEPTH | L: o_proj / down_proj of an L-layer model under the

@@ -14,6 +14,8 @@ reference's bars are demanded literally here -- a divergence is accepted only
 at an fp32-level tie (the oracle's gap between the two picks <= 1e-4, reported
 if it ever happens).
 """
+import ctypes
+
 import numpy as np
 import pytest
 
@@ -55,6 +57,69 @@ def test_linear_f32_against_fp64(T, N, K):
     err = np.abs(y1 - ref)
     assert np.all(err <= 2e-6 * mag + 1e-30), float((err / mag).max())
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
+
+
+def ulps32(a, b):
+    """distance in fp32 ulps (monotonic int mapping)"""
+    def key(x):
+        u = np.asarray(x, np.float32).view(np.int32).astype(np.int64)
+        return np.where(u < 0, -(u & 0x7FFFFFFF), u)
+    return np.abs(key(a) - key(b))
+
+
+@pytest.mark.parametrize("H", [768, 4096])
+def test_rmsnorm_f32_against_oracle(H):
+    """ffmi_rmsnorm_f32 / ffmi_residual_rmsnorm_f32 vs the oracle's fp32 mode
+    (the same fp32 operations; only the fp64 sum of squares is reordered):
+    within 1 ulp, >= 99% bit-identical, the residual sum bit-exact"""
+    rng = np.random.default_rng(H)
+    T, eps = 13, 1e-6
+    x1 = rng.standard_normal((T, H)).astype(np.float32)
+    x2 = rng.standard_normal((T, H)).astype(np.float32)
+    w = rng.uniform(0.5, 1.5, H).astype(np.float32)
+    L = F.lib()
+    b1, b2, bw = Buf(x1), Buf(x2), Buf(w)
+    out, res = Buf.empty((T, H), np.float32), Buf.empty((T, H), np.float32)
+    assert L.ffmi_rmsnorm_f32(b1.ptr, bw.ptr, out.ptr, T, H, ctypes.c_float(eps), None) == 0
+    d = ulps32(out.get(), O.rmsnorm(x1, w, eps, fp16=0))
+    assert d.max() <= 1 and (d == 0).mean() >= 0.99, (int(d.max()), float((d == 0).mean()))
+    assert L.ffmi_residual_rmsnorm_f32(b1.ptr, b2.ptr, bw.ptr, res.ptr, out.ptr, T, H,
+                                       ctypes.c_float(eps), None) == 0
+    rr, ro = O.residual_rmsnorm(x1, x2, w, eps, fp16=0)
+    assert np.array_equal(res.get(), rr)
+    d = ulps32(out.get(), ro)
+    assert d.max() <= 1 and (d == 0).mean() >= 0.99
+
+
+def test_silu_mul_f32_against_oracle():
+    """SigmoidSiluMulti on fp32: the device expf against the host's (each
+    within ~1 ulp of exp) carried through 1/(1 + e), a * sg and * b: <= 4 ulp,
+    >= 90% bit-identical"""
+    rng = np.random.default_rng(9)
+    a = (4 * rng.standard_normal(50000)).astype(np.float32)
+    b = rng.standard_normal(50000).astype(np.float32)
+    ba, bb, bo = Buf(a), Buf(b), Buf.empty((50000,), np.float32)
+    assert F.lib().ffmi_silu_mul_f32(ba.ptr, bb.ptr, bo.ptr, 50000, None) == 0
+    d = ulps32(bo.get(), O.silu_mul(a, b, fp16=0))
+    assert d.max() <= 4 and (d == 0).mean() >= 0.9, (int(d.max()), float((d == 0).mean()))
+
+
+@pytest.mark.parametrize("k", [1, 3])
+def test_arg_topk_f32_against_oracle(k):
+    """softmax + arg-top-k on fp32 probabilities, lowest index among equal
+    probabilities (planted exact ties, also across the top-k boundary)"""
+    rng = np.random.default_rng(k)
+    T, V = 24, 32000
+    z = rng.standard_normal((T, V)).astype(np.float32)
+    for t in range(0, T, 3):  # ties: the row's max copied to a lower and a higher index
+        j = int(z[t].argmax())
+        z[t, (j + 7) % V] = z[t, j]
+        z[t, (j + V - 5) % V] = z[t, j]
+    bz, bi, bp = Buf(z), Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+    assert F.lib().ffmi_arg_topk_f32(bz.ptr, T, V, k, bi.ptr, bp.ptr, None) == 0
+    ids, probs = O.softmax_topk(z, k, fp16=0)
+    assert np.array_equal(bi.get(), ids)
+    assert ulps32(bp.get(), probs).max() <= 2
 
 
 def oracle_greedy(om, prompts, n_new):
