@@ -41,12 +41,22 @@ def _child(rank, n, conn, task, args, env, max_bytes, device):
 
 def run_group(n, task, args=(), env=None, max_bytes=1 << 22, timeout=240, device=0):
     """Run task(fa, comm, rank, n, *args) on n ranks; returns [result per rank].
-    A rank that fails, or a group that exceeds `timeout`, raises."""
+    A rank that fails, or a group that exceeds `timeout`, raises.
+
+    Each rank gets GPU_MAX_HW_QUEUES=1 unless `env` says otherwise: n processes
+    with HIP's default of up to 4 hardware queues each (their compute and
+    all-reduce streams) oversubscribe the device's queue slots, the scheduler
+    then time-slices between processes, and every all-reduce waits out the
+    slices of the peers it spins on (8 ranks of the 7B bench: 370 s per
+    generate; with one queue per rank 7.6 s).  One queue serialises a rank's
+    two streams in issue order -- the cross-stream waits still hold, only the
+    overlap is gone -- which changes no value."""
+    env = {"GPU_MAX_HW_QUEUES": "1", **(env or {})}
     ctx = mp.get_context("spawn")
     pipes, procs = [], []
     for r in range(n):
         a, b = ctx.Pipe()
-        p = ctx.Process(target=_child, args=(r, n, b, task, args, env or {}, max_bytes, device))
+        p = ctx.Process(target=_child, args=(r, n, b, task, args, env, max_bytes, device))
         p.start()
         pipes.append(a)
         procs.append(p)
