@@ -191,8 +191,6 @@ def cpu_baseline(acceptance=1.0, prompt_len=128, batch=8, budget_s=12.0, incr_bu
     first prompt_len KV rows hold zeros, so this is a timing sample (every
     step reads as many keys as the GPU run's), not a token replay."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import numpy as np
-
     import oracle_lib as O
     tree = 21  # 1 root + layers 1, 1, 3 x 6 (widths (1,1,3), 8 SSM steps)
     layer_sizes = [1, 1, 3, 3, 3, 3, 3, 3]

@@ -5,7 +5,7 @@ runtime and HIP kernels; this file only marshals arguments.
 """
 import ctypes
 import os
-from dataclasses import dataclass, field
+from dataclasses import dataclass
 from typing import List, Optional, Union
 
 from . import ffmi as F

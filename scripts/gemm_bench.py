@@ -3,7 +3,6 @@
     python scripts/gemm_bench.py [--shapes llama7b|ssm] [--T 1,8,168]
 """
 import argparse
-import ctypes
 import json
 import os
 import sys

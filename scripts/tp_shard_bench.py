@@ -13,14 +13,13 @@ communicator, which now takes the RCCL path and times ncclAllReduce calls.)
 import argparse
 import json
 import os
-import statistics
 import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import flexflow_amd as fa  # noqa: E402
-from bench import LLAMA_65B, LLAMA_68M, LLAMA_7B, make_prompts, stdout_to_stderr  # noqa: E402
+from bench import LLAMA_65B, LLAMA_68M, LLAMA_7B, make_prompts  # noqa: E402
 
 
 def main():

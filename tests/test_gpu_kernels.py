@@ -13,7 +13,7 @@ import pytest
 
 import flexflow_amd.ffmi as F
 import oracle_lib as O
-from hip_util import Buf, f16, hip, sync, ulp_diff
+from hip_util import Buf, f16, hip, ulp_diff
 
 pytestmark = pytest.mark.gpu
 
