@@ -481,7 +481,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     if constexpr (OP) {
 #pragma unroll
       for (int j = 0; j < OT; ++j) {
-        const int t = wave + j * NW;
+        const int t = (wave + j * NW) * (int)gridDim.z + (int)blockIdx.z;  // (column split)
         if (t < o_tiles) {
 #pragma unroll
           for (int ks = 0; ks < KS; ++ks)
@@ -819,7 +819,7 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
     float *srow = opa.slab + ((size_t)h * kv.T + w.q_start + qi) * opa.N + 4 * g;
 #pragma unroll
     for (int j = 0; j < OT; ++j) {
-      const int t = wave + j * NW;
+      const int t = (wave + j * NW) * (int)gridDim.z + (int)blockIdx.z;
       if (t < o_tiles) {
         f4 c = f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -839,7 +839,8 @@ __global__ __launch_bounds__(64 * NW, 1) void attention_kernel(
 // queries per item: when the (item, head) grid leaves half the CUs idle
 // (TP >= 2 verify steps).  FFMI_ATTN_QSPLIT: 0 off, 1 auto (default), 2
 // always (tests; read at every launch, so a test can switch it).
-static bool attn_qsplit(int wgs) {
+// a doubled grid still fits one wave of the device's CUs
+static bool attn_split_fits(int wgs) {
   static int cus = 0;
   if (!cus) {
     int dev = 0;
@@ -847,9 +848,19 @@ static bool attn_qsplit(int wgs) {
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
       cus = 256;
   }
+  return 2 * wgs <= cus;
+}
+
+static bool attn_qsplit(int wgs) {
   const char *e = getenv("FFMI_ATTN_QSPLIT");
   const int mode = e ? atoi(e) : 1;
-  return mode == 2 || (mode == 1 && 2 * wgs <= cus);
+  return mode == 2 || (mode == 1 && attn_split_fits(wgs));
+}
+
+static bool attn_osplit(int wgs) {
+  const char *e = getenv("FFMI_ATTN_OSPLIT");
+  const int mode = e ? atoi(e) : 1;
+  return mode == 2 || (mode == 1 && attn_split_fits(wgs));
 }
 
 template <int D>
@@ -980,7 +991,14 @@ hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, 
   if (opa) {  // output projection folded in (the caller checked fused, d, max_q, N)
     if (!fused || d != 64 || max_q > 16 || opa->N % 16 || opa->N > 16 * 8 * 8 || T > opa->max_T)
       return hipErrorInvalidValue;
-    const dim3 grid(W, heads);
+    // output-column split: when the (item, head) grid leaves half the CUs
+    // idle (the 68M SSM: 8 x 12 = 96 workgroups), two workgroups per (item,
+    // head) each project half of the column tiles; both attend and run the
+    // KV update (the same values to the same addresses, as the query split).
+    // The projection's weight slice (96 KiB) and MFMAs per workgroup halve:
+    // SSM step 102.9 -> 100.4 us over 5 same-box pairs (profiles/r04_attn_osplit_ab.log).
+    // FFMI_ATTN_OSPLIT: 0 off, 1 auto (default), 2 always (read per launch).
+    const dim3 grid(W, heads, attn_osplit(W * heads) ? 2 : 1);
     if (kv.part)
       hipLaunchKernelGGL((attention_kernel<64, 1, 8, true, false, 1, true>), grid, dim3(512), 0, s,
                          blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, *opa);

@@ -341,6 +341,30 @@ SSM68_CFG = dict(num_layers=2, vocab_size=1000, num_heads=12, num_kv_heads=12, h
                  intermediate=1024, rms_eps=1e-6, rope_theta=10000.0)
 
 
+def test_attention_oproj_column_split_bit_identical(monkeypatch):
+    """The fused o projection's output-column split (two workgroups per
+    (request, head), each projecting half of the column tiles;
+    FFMI_ATTN_OSPLIT 2 = always, 0 = off) computes every tile with the same
+    MFMA chain: captured attention outputs, o_proj and tokens bit-identical."""
+    cfg, seed = SSM68_CFG, 9
+    ps = prompts(4, cfg["vocab_size"], 5, 40, seed)
+    runs = []
+    for mode in ("2", "0"):
+        monkeypatch.setenv("FFMI_ATTN_OSPLIT", mode)
+        m = fa.Model(cfg, "inc", max_requests=4, max_tokens=64, max_seq_len=128, weight_seed=seed)
+        m.set_debug(True)
+        res = fa.generate(fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=64,
+                                            max_sequence_length=128), m, ps, max_length=48)
+        cap = [m.debug_tensor(op, l) for l in range(cfg["num_layers"])
+               for op in ("attn_out", "o_proj", "hidden")]
+        runs.append((cap, [r.output_tokens for r in res]))
+        del m
+    (a, ta), (b, tb) = runs
+    assert ta == tb
+    for x, y in zip(a, b):
+        assert np.array_equal(x.view(np.uint32), y.view(np.uint32))
+
+
 @pytest.mark.parametrize("cfg,seed", [(SSM68_CFG, 9), (SSM_CFG, 5)])
 def test_attention_oproj_equals_o_gemm(monkeypatch, cfg, seed):
     """The o projection folded into the fused attention (OprojArgs: d = 64,
