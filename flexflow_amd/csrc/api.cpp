@@ -42,7 +42,9 @@ extern "C" const char *ffmi_status_str(ffmi_status s) {
   return "unknown";
 }
 
-extern "C" const char *ffmi_version(void) { return "ffmi 0.1 (gfx950)"; }
+// 0.2: ffmi_attn_cfg.full_precision and ffmi_model_opts.full_precision
+// appended (struct sizes changed), the *_f32 entry points added
+extern "C" const char *ffmi_version(void) { return "ffmi 0.2 (gfx950)"; }
 
 // ---------------------------------------------------------------------------
 // batch metadata

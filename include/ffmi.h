@@ -532,6 +532,8 @@ long ffmi_debug_markers(long long *dst, long n);
 const char *ffmi_status_str(ffmi_status s);
 /* message + file:line of the last failing check on this process */
 const char *ffmi_last_error(void);
+/* "ffmi 0.2 (gfx950)": 0.2 appended full_precision to ffmi_attn_cfg and
+ * ffmi_model_opts (struct sizes changed) and added the *_f32 entry points */
 const char *ffmi_version(void);
 
 #ifdef __cplusplus
