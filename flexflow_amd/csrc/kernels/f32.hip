@@ -15,6 +15,8 @@
 //  * softmax + argmax / arg-top-k on fp32 probabilities (softmax.cu:262-288,
 //    argmax.cu:62-100, arg_topk.cu:339-448): lowest index among equal maxima.
 // KV cache fp32, K[req][head][slot][d] and V[req][head][slot][d].
+#include <stdlib.h>
+
 #include <algorithm>
 
 #include "../ffmi_internal.h"
@@ -136,8 +138,16 @@ hipError_t launch_gemm_f32(const float *X, const float *W, float *Y, int T, int 
     hipLaunchKernelGGL((f32_gemm_kernel<4, 1, 1, 1, 4>), dim3((N + 15) / 16, 1), dim3(256), 0, s, X, W,
                        Y, T, N, K);
   } else {
-    hipLaunchKernelGGL((f32_gemm_kernel<2, 2, 2, 2, 1>), dim3((N + 63) / 64, (T + 63) / 64),
-                       dim3(256), 0, s, X, W, Y, T, N, K);
+    // 64 x 64 output tile per wave, K split over the workgroup's 4 waves: per
+    // MFMA half the operand bytes of 32 x 32 wave tiles at the same grid
+    // (FFMI_F32_GEMM_TILE=1: the 2 x 2-wave, 32 x 32-per-wave form, A/B)
+    static const bool tile = getenv("FFMI_F32_GEMM_TILE") && atoi(getenv("FFMI_F32_GEMM_TILE"));
+    if (tile)
+      hipLaunchKernelGGL((f32_gemm_kernel<2, 2, 2, 2, 1>), dim3((N + 63) / 64, (T + 63) / 64),
+                         dim3(256), 0, s, X, W, Y, T, N, K);
+    else
+      hipLaunchKernelGGL((f32_gemm_kernel<4, 4, 1, 1, 4>), dim3((N + 63) / 64, (T + 63) / 64),
+                         dim3(256), 0, s, X, W, Y, T, N, K);
   }
   return hipGetLastError();
 }
