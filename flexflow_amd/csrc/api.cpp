@@ -44,7 +44,8 @@ extern "C" const char *ffmi_status_str(ffmi_status s) {
 
 // 0.2: ffmi_attn_cfg.full_precision and ffmi_model_opts.full_precision
 // appended (struct sizes changed), the *_f32 entry points added
-extern "C" const char *ffmi_version(void) { return "ffmi 0.2 (gfx950)"; }
+// 0.3: ffmi_rm_config.spec_extensions
+extern "C" const char *ffmi_version(void) { return "ffmi 0.3 (gfx950)"; }
 
 // ---------------------------------------------------------------------------
 // batch metadata
@@ -334,9 +335,11 @@ ffmi_status attn_rope_fault(ffmi_attn *h, int from_pos) {
   std::vector<float> tab;
   rope_table(tab, h->slots + 1, h->cfg.head_dim, &h->cfg);
   const size_t row = (size_t)h->cfg.head_dim;
+  // ascending: row p takes row p + 1 before row p + 1 itself is shifted, so
+  // every position >= from_pos rotates as exactly position + 1
   if (from_pos >= 0)
-    for (int p = h->slots - 1; p >= std::max(from_pos, 0); --p)
-      memcpy(&tab[p * row], &tab[(p + 1) * row], row * sizeof(float));
+    for (int p = from_pos; p < h->slots; ++p)
+      memcpy(&tab[(size_t)p * row], &tab[(size_t)(p + 1) * row], row * sizeof(float));
   FFMI_HIP(hipMemcpy(h->rope, tab.data(), (size_t)h->slots * row * sizeof(float),
                      hipMemcpyHostToDevice));
   return FFMI_OK;

@@ -92,9 +92,16 @@ class BeamSearchBatchConfig : public BatchConfig {
   int current_depth_all_requests() const;
   int get_speculative_request_num() const { return speculative_request_num; }
 
-  static constexpr int MAX_BEAM_WIDTH = 3;
+  // Capacities.  The reference's limits are 3 and 3 (batch_config.h:196,200,
+  // enforced by push_spec_infer_tree_width, request_manager.cc:168-171); the
+  // arrays here hold 4 so that the flagged tree-width-4 extension
+  // (FFMI_SPEC_EXT_WIDTH4, BASELINE config C) fits.  RequestManager enforces
+  // the reference's 3 unless that flag is set.
+  static constexpr int MAX_BEAM_WIDTH = 4;
   static constexpr int MAX_BEAM_DEPTH = 8;
-  static constexpr int MAX_SPECULATIVE_TREE_BRANCHES = 3;
+  static constexpr int MAX_SPECULATIVE_TREE_BRANCHES = 4;
+  static constexpr int REFERENCE_MAX_BEAM_WIDTH = 3;
+  static constexpr int REFERENCE_MAX_SPECULATIVE_TREE_BRANCHES = 3;
 
   int speculative_request_num = 0;
   int model_id = 0;
@@ -102,9 +109,9 @@ class BeamSearchBatchConfig : public BatchConfig {
     int beam_size = 1;
     int current_depth = -1;
     int max_depth = MAX_BEAM_DEPTH;
-    TokenId tokens[MAX_SPECULATIVE_TREE_BRANCHES] = {0, 0, 0};
-    float probs[MAX_SPECULATIVE_TREE_BRANCHES] = {0, 0, 0};
-    int parent_id[MAX_SPECULATIVE_TREE_BRANCHES] = {0, 0, 0};
+    TokenId tokens[MAX_SPECULATIVE_TREE_BRANCHES] = {};
+    float probs[MAX_SPECULATIVE_TREE_BRANCHES] = {};
+    int parent_id[MAX_SPECULATIVE_TREE_BRANCHES] = {};
     int sub_request_num = 0;
   };
   struct BeamSearchPerTokenInfo {

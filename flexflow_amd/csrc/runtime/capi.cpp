@@ -87,10 +87,16 @@ extern "C" ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out) 
   std::vector<int> eos;
   for (int i = 0; i < cfg->num_eos; ++i) eos.push_back(cfg->eos_token_ids[i]);
   r->rm.register_tokenizer(cfg->bos_token_id, eos);
+  if (cfg->spec_extensions & ~(FFMI_SPEC_EXT_WIDTH4 | FFMI_SPEC_EXT_MULTI_SSM)) {
+    delete r;
+    return FFMI_ERR_INVALID;
+  }
+  r->rm.set_spec_extensions(cfg->spec_extensions);
   for (int i = 0; i < cfg->num_tree_width; ++i)
     if (!r->rm.push_spec_infer_tree_width(cfg->spec_tree_width[i])) {
       delete r;
-      return FFMI_ERR_INVALID;  // tree_width <= MAX_BEAM_WIDTH (request_manager.cc:168-171)
+      return FFMI_ERR_INVALID;  // tree_width <= MAX_BEAM_WIDTH (request_manager.cc:168-171),
+                                // 4 under FFMI_SPEC_EXT_WIDTH4
     }
   r->rm.set_verbose(cfg->verbose != 0);
   *out = r;

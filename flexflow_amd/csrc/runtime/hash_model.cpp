@@ -91,11 +91,12 @@ struct HashModel : public ffmi_model {
       const int c0 = next_token(h);
       const int c1 = (int)((c0 + 1 + (h >> 40) % 7) % (uint64_t)vocab);
       const int c2 = (int)((c1 + 1 + (h >> 45) % 7) % (uint64_t)vocab);
+      const int c3 = (int)((c2 + 1 + (h >> 50) % 7) % (uint64_t)vocab);  // k = 4 (width 4)
       const bool agree = (int)(mix64(h ^ salt) % 100) >= disagree;
-      std::array<int, 3> rank = agree ? std::array<int, 3>{c0, c1, c2}
-                                      : std::array<int, 3>{c1, c0, c2};
+      std::array<int, 4> rank = agree ? std::array<int, 4>{c0, c1, c2, c3}
+                                      : std::array<int, 4>{c1, c0, c2, c3};
       for (int j = 0; j < k; ++j) {
-        ir->token_ids[t * k + j] = rank[j % 3];
+        ir->token_ids[t * k + j] = rank[j % 4];
         ir->probs[t * k + j] = 1.0f / (float)(1 << j);
         ir->parent_id[t * k + j] = 0;
       }
@@ -107,7 +108,7 @@ struct HashModel : public ffmi_model {
 ffmi_status create_hash_model(int vocab, int mode, int max_requests, int max_seq,
                               int max_tree, uint64_t salt, int disagree_pct,
                               ffmi_model **out) {
-  if (vocab < 16 || max_requests <= 0 || max_seq <= 0) return FFMI_ERR_INVALID;
+  if (vocab < 32 || max_requests <= 0 || max_seq <= 0) return FFMI_ERR_INVALID;
   HashModel *m = new HashModel();
   m->mode = mode;
   m->vocab = vocab;

@@ -62,6 +62,21 @@ struct LlamaF32 : public ffmi_model {
     if (stream) (void)hipStreamDestroy(stream);
   }
 
+  // FFMI_FAULT_ROPE_POS / FFMI_FAULT_NONE on the DT_FLOAT handles' RoPE tables
+  // (the negative control of the full-precision bars; include/ffmi.h)
+  ffmi_status debug_fault(int kind, int layer, int arg) override {
+    if (stream) FFMI_HIP(hipStreamSynchronize(stream));
+    FFMI_CHECK(kind == FFMI_FAULT_NONE ||
+                   (kind == FFMI_FAULT_ROPE_POS && layer >= -1 && layer < c.num_layers),
+               FFMI_ERR_INVALID);
+    for (int l = 0; l < c.num_layers; ++l)
+      if (kind == FFMI_FAULT_NONE || layer < 0 || l == layer) {
+        ffmi_status st = ffmi::attn_rope_fault(layers[l].attn, kind == FFMI_FAULT_NONE ? -1 : arg);
+        if (st != FFMI_OK) return st;
+      }
+    return FFMI_OK;
+  }
+
   template <typename T>
   ffmi_status alloc(T **p, size_t elems) {
     if (hipMalloc((void **)p, elems * sizeof(T)) != hipSuccess) {

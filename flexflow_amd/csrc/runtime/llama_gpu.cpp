@@ -294,6 +294,9 @@ struct LlamaGPU : public ffmi_model {
   }
 
   ffmi_status debug_fault(int kind, int layer, int arg) override {
+    // the tables are rewritten with blocking copies: finish the model's
+    // (non-blocking) stream first in every branch
+    if (stream) FFMI_HIP(hipStreamSynchronize(stream));
     if (kind == FFMI_FAULT_NONE) {
       for (auto &L : layers) {
         ffmi_status st = ffmi::attn_rope_fault(L.attn, -1);
@@ -303,7 +306,6 @@ struct LlamaGPU : public ffmi_model {
     }
     FFMI_CHECK(kind == FFMI_FAULT_ROPE_POS && layer >= -1 && layer < c.num_layers,
                FFMI_ERR_INVALID);
-    if (stream) FFMI_HIP(hipStreamSynchronize(stream));
     for (int l = 0; l < c.num_layers; ++l)
       if (layer < 0 || l == layer) {
         ffmi_status st = ffmi::attn_rope_fault(layers[l].attn, arg);

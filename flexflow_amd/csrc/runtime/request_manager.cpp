@@ -6,8 +6,13 @@
 //    `1 << j` on int breaks for trees deeper than 31 tokens (quirk 6);
 //  * no tokenizer: requests carry token ids (the parity unit);
 //  * no PEFT / finetuning requests;
-//  * more than one SSM is rejected, as the reference asserts
-//    (merge_dfs_trees, request_manager.cc:2823-2827).
+//  * flagged extensions (FFMI_SPEC_EXT_*, off by default, where the reference
+//    asserts): tree width / branches 4 (request_manager.cc:168-171 allows 3),
+//    and N SSMs whose trees merge_dfs_trees unites (the reference asserts one
+//    SSM, :2823-2827, ahead of a merge it never runs);
+//  * the verify step walks the tree by parent links (traverse_verify_tree):
+//    identical to the reference's layer-slot walk on every tree it admits,
+//    and correct on trees that branch twice or are merged.
 #include "request_manager.h"
 
 #include <assert.h>
@@ -15,6 +20,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <map>
 
 void ffmi_set_last_error(const char *msg, const char *file, int line);  // api.cpp
 
@@ -59,15 +65,25 @@ void RequestManager::apply_limits() const {
   g_limits.max_sequence_length = max_sequence_length;
 }
 
+int RequestManager::max_beam_width() const {
+  return spec_extensions & FFMI_SPEC_EXT_WIDTH4 ? BeamSearchBatchConfig::MAX_BEAM_WIDTH
+                                                : BeamSearchBatchConfig::REFERENCE_MAX_BEAM_WIDTH;
+}
+int RequestManager::max_tree_branches() const {
+  return spec_extensions & FFMI_SPEC_EXT_WIDTH4
+             ? BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES
+             : BeamSearchBatchConfig::REFERENCE_MAX_SPECULATIVE_TREE_BRANCHES;
+}
+
 // request_manager.cc:168-171
 bool RequestManager::push_spec_infer_tree_width(int w) {
-  if (w > BeamSearchBatchConfig::MAX_BEAM_WIDTH || w < 1) return false;
+  if (w > max_beam_width() || w < 1) return false;
   // nodes per tree layer = product of the widths so far; the reference
   // asserts it stays <= MAX_SPECULATIVE_TREE_BRANCHES at run time
   // (request_manager.cc:1685-1687) -- reject such a sequence up front
   int nodes = w;
   for (int x : spec_infer_tree_width) nodes *= x;
-  if (nodes > BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES) return false;
+  if (nodes > max_tree_branches()) return false;
   spec_infer_tree_width.push_back(w);
   return true;
 }
@@ -321,6 +337,7 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
         new_bc.request_completed[i] = true;
         new_bc.request_running[i] = false;
         dfs_tree_inputs.erase(guid);
+        dfs_tree_parents.erase(guid);
       } else {
         new_bc.request_completed[i] = false;
         new_bc.request_running[i] = true;
@@ -463,7 +480,12 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_beam(
     R.first_token_offset_in_batch = new_bc.num_tokens;
     R.request_guid = old_bc.requestsInfo[i].request_guid;
     R.max_length = old_bc.requestsInfo[i].max_length;
-    const int steps = ++profiling_requests[request.guid].ssm_decoding_steps;
+    ++profiling_requests[request.guid].ssm_decoding_steps;
+    // the reference indexes the widths by ssm_decoding_steps, reset to 0 at
+    // init and counted per beam batch (:1680-1683): with one SSM that is
+    // the beam depth reached, OB.current_depth.  With N SSMs the counter runs
+    // on through every SSM's steps, so the depth is used.
+    const int steps = OB.current_depth;
     new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
     B.beam_size = (int)spec_infer_tree_width.size() > steps ? spec_infer_tree_width[steps] : 1;
     B.max_depth = OB.max_depth;
@@ -526,7 +548,8 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_beam(
       R.num_tokens_in_batch =
           std::min(max_tokens_per_batch - new_bc.num_tokens - max_requests_per_batch + i,
                    (int)request.tokens.size() - R.first_token_depth_in_request);
-      request.ssm_cache_size += R.num_tokens_in_batch;
+      // every SSM loads the same prompt chunk; count it once
+      if (old_bc.model_id == 0) request.ssm_cache_size += R.num_tokens_in_batch;
       appendPendingRequest(new_bc.causalMask[i], R.num_tokens_in_batch);
     }
     for (int j = 0; j < R.num_tokens_in_batch; j++) {
@@ -580,6 +603,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
             traverse_beam_tree(old_batches.at(j), i, (int)request.tokens.size() - 1));
       std::vector<TokenDepth> tree =
           merge_dfs_trees(all_dfs_trees, (int)request.tokens.size() - 1, guid);
+      const std::vector<int> &parent = dfs_tree_parents.at(guid);
       R.first_token_depth_in_request = tree.front().second;
       R.first_token_offset_in_batch = new_bc.num_tokens;
       R.request_guid = guid;
@@ -630,6 +654,10 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
             break;
         }
       }
+      // the verify bitmask of the tree as placed (a layer-order prefix of it
+      // after cutLayer).  With one SSM this is the mask its beam steps built
+      // (appendBitMask, :2426-2476); a merged tree needs its own.
+      tree_bitmask(parent, R.num_tokens_in_batch, new_bc.causalMask[i]);
       stats.tree_tokens_verified += R.num_tokens_in_batch;
     } else if (request.status == Request::PENDING) {
       new_bc.request_running[i] = false;
@@ -668,6 +696,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
           R.prompt_phase = true;
           dfs_tree_inputs[guid] = std::vector<TokenDepth>{
               TokenDepth(request.tokens.back(), (int)request.tokens.size() - 1)};
+          dfs_tree_parents[guid] = std::vector<int>{-1};
         }
       } else if (max_verify - new_bc.num_tokens > 0) {
         // whole prompt cached: launch the request with its last token
@@ -682,6 +711,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
         R.prompt_phase = true;
         dfs_tree_inputs[guid] = std::vector<TokenDepth>{
             TokenDepth(request.tokens.back(), (int)request.tokens.size() - 1)};
+        dfs_tree_parents[guid] = std::vector<int>{-1};
       }
     } else {
       assert(false && "request status is not RUNNING or PENDING");
@@ -806,59 +836,45 @@ void RequestManager::appendBitMask(BatchConfig::BitMask &bitmask, int newNodes,
   for (int i = token_idx; i < bitmask.tree_size; i++) bitmask.mask[i] |= (1ull << i);
 }
 
-// request_manager.cc:2583-2741: greedy path acceptance over the layer-order
-// serialized tree; returns the verified (token, depth) list and rewrites the
-// request's commit list to the accepted nodes.
+// request_manager.cc:2583-2741: greedy path acceptance; returns the
+// verified (token, depth) list and rewrites the request's commit list to the
+// accepted nodes.  output[i] is the LLM's pick at tree node i.  Node c is
+// accepted when its parent is the last accepted node and its token is the
+// LLM's pick there.  The reference walks the layer-order list instead and,
+// once a node of a branching layer matched, accepts only the same slot of
+// every later layer (:2665-2700); on the trees it admits (widths whose
+// product is <= 3: one branching layer, chains below it) that slot IS the
+// accepted node's only child, so both walks accept the same nodes.  Trees that
+// branch twice (widths (2, 2) under FFMI_SPEC_EXT_WIDTH4) and merged trees
+// need the parent links.
 std::vector<RequestManager::TokenDepth> RequestManager::traverse_verify_tree(
     size_t guid, const std::vector<TokenDepth> &input, const std::vector<TokenDepth> &output) {
   std::vector<TokenDepth> verifiedTree;
   std::vector<std::pair<int, int>> new_committed_tokens;
   assert(input.size() >= output.size());
-  std::vector<int> treeLayers(input.size());
-  int node_num = 1, layer_num = 0;
-  for (size_t t = 0; t < input.size(); t++) {
-    if (t == input.size() - 1 || input.at(t + 1).second != input.at(t).second) {
-      treeLayers[layer_num++] = node_num;
-      node_num = 1;
-    } else {
-      node_num++;
+  const RequestGuid g = (RequestGuid)guid;
+  auto pit = dfs_tree_parents.find(g);
+  const std::vector<int> parent = pit != dfs_tree_parents.end() && pit->second.size() == input.size()
+                                      ? pit->second
+                                      : layer_order_parents(input);
+  const auto &ct = committed_tokens.at(g);
+  if (!output.empty()) {
+    assert(ct.at(0).first == input.at(0).second);
+    verifiedTree.push_back(output[0]);
+    new_committed_tokens.push_back(std::make_pair(input[0].second, ct.at(0).second));
+    int last = 0;
+    for (size_t c = 1; c < output.size(); ++c) {
+      if (parent[c] != last) continue;
+      if (input[c].first != verifiedTree.back().first ||
+          input[c].second != verifiedTree.back().second)
+        continue;
+      assert(ct.at(c).first == input[c].second);
+      verifiedTree.push_back(output[c]);
+      new_committed_tokens.push_back(std::make_pair(input[c].second, ct.at(c).second));
+      last = (int)c;
     }
   }
-  bool findFirst = false;
-  layer_num = -1;
-  int first_layer_slot = 0;
-  int processed_whole_layer_tokens = 0;
-  const auto &ct = committed_tokens.at((RequestGuid)guid);
-  for (size_t i = 0; i < output.size(); i++) {
-    const auto &in = input.at(i);
-    const auto &out = output.at(i);
-    if (i == 0 || input.at(i - 1).second != input.at(i).second) {
-      layer_num += 1;
-      processed_whole_layer_tokens += i == 0 ? 0 : treeLayers[layer_num - 1];
-    }
-    if (i == 0) {
-      verifiedTree.push_back(out);
-      new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
-      assert(ct.at(i).first == in.second);
-      continue;
-    }
-    if (in.first == verifiedTree.back().first && in.second == verifiedTree.back().second) {
-      if (findFirst) {
-        const int layer_slot = (int)i - processed_whole_layer_tokens;
-        if (first_layer_slot == layer_slot) {
-          verifiedTree.push_back(out);
-          new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
-        }
-      } else {
-        verifiedTree.push_back(out);
-        first_layer_slot = (int)i - processed_whole_layer_tokens;
-        findFirst = true;
-        new_committed_tokens.push_back(std::make_pair(in.second, ct.at(i).second));
-      }
-      assert(ct.at(i).first == in.second);
-    }
-  }
-  committed_tokens[(RequestGuid)guid] = new_committed_tokens;
+  committed_tokens[g] = new_committed_tokens;
   return verifiedTree;
 }
 
@@ -876,13 +892,93 @@ std::vector<RequestManager::TokenDepth> RequestManager::traverse_beam_tree(
   return serializedTree;
 }
 
-// request_manager.cc:2817-2878 (one SSM: the tree is used as is)
+std::vector<int> RequestManager::layer_order_parents(const std::vector<TokenDepth> &tree) {
+  std::vector<int> parent(tree.size(), -1);
+  size_t prev_start = 0, prev_n = 0;
+  for (size_t i = 0; i < tree.size();) {
+    size_t j = i;
+    while (j < tree.size() && tree[j].second == tree[i].second) ++j;
+    const size_t n = j - i;
+    if (i > 0)  // n_d = n_{d-1} * width: equal groups (store_beam_metadata, :2304-2316)
+      for (size_t k = 0; k < n; ++k) parent[i + k] = (int)(prev_start + k * prev_n / n);
+    prev_start = i;
+    prev_n = n;
+    i = j;
+  }
+  return parent;
+}
+
+void RequestManager::tree_bitmask(const std::vector<int> &parent, int n,
+                                  BatchConfig::BitMask &m) {
+  assert(n <= BatchConfig::MAX_SPEC_TREE_TOKEN_NUM && n <= (int)parent.size());
+  std::fill(m.mask, m.mask + BatchConfig::MAX_SPEC_TREE_TOKEN_NUM, 0ull);
+  for (int q = 0; q < n; ++q)
+    for (int a = q; a >= 0; a = parent[a]) m.mask[a] |= 1ull << q;
+  m.tree_size = n;
+}
+
+// request_manager.cc:2817-2878.  One SSM: its tree is used as is (the
+// reference's path).  N SSMs (FFMI_SPEC_EXT_MULTI_SSM): the reference's merge
+// after its assert gives every node the id token * 10000 + depth, records
+// each node under curr_path[depth - 1] as its parent's child and emits the
+// union depth-first from the root.  Restated here with two corrections: a
+// node's identity is its PATH from the root (the <token, depth> id joins two
+// different nodes that carry the same token at the same depth, giving the
+// union node two parents, whose KV contexts differ), and the parent of a node
+// comes from the layer-order grouping its SSM built (curr_path presumes the
+// depth-first serialisation traverse_beam_tree no longer produces).  The union
+// is emitted in layer order (depth, then first-seen: SSM 0's nodes, then new
+// nodes of SSM 1, ...), the order the verify step, its bitmask and the commit
+// lists use, and is cut to max_spec_tree_token_num nodes (<= 64, the
+// bitmask's width): a layer-order prefix, so every kept node keeps its
+// ancestors.
 std::vector<RequestManager::TokenDepth> RequestManager::merge_dfs_trees(
     const std::vector<std::vector<TokenDepth>> &trees, int root_depth, RequestGuid guid) {
   (void)root_depth;
-  assert(trees.size() == 1 && "currently using one ssm");
-  dfs_tree_inputs[guid] = trees.at(0);
-  return trees.at(0);
+  assert(!trees.empty());
+  if (trees.size() == 1) {
+    dfs_tree_inputs[guid] = trees[0];
+    dfs_tree_parents[guid] = layer_order_parents(trees[0]);
+    return trees[0];
+  }
+  struct Node {
+    TokenDepth td;
+    int parent;
+  };
+  std::vector<Node> nodes;
+  std::map<std::pair<int, int>, int> child;  // (parent id, token) -> node id
+  const TokenDepth root = trees[0].at(0);
+  nodes.push_back(Node{root, -1});
+  for (const auto &tree : trees) {
+    assert(!tree.empty() && tree[0] == root);  // all trees share the root
+    const std::vector<int> par = layer_order_parents(tree);
+    std::vector<int> id(tree.size(), 0);
+    for (size_t i = 1; i < tree.size(); ++i) {
+      const int p = id[par[i]];
+      auto ins = child.emplace(std::make_pair(p, tree[i].first), (int)nodes.size());
+      if (ins.second) nodes.push_back(Node{tree[i], p});
+      id[i] = ins.first->second;
+    }
+  }
+  std::vector<int> order(nodes.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
+    return nodes[a].td.second < nodes[b].td.second;
+  });
+  const int cap = std::max(1, std::min(max_spec_tree_token_num,
+                                       (int)BatchConfig::MAX_SPEC_TREE_TOKEN_NUM));
+  if ((int)order.size() > cap) order.resize(cap);
+  std::vector<int> pos(nodes.size(), -1);
+  for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
+  std::vector<TokenDepth> merged;
+  std::vector<int> mparent;
+  for (int id : order) {
+    merged.push_back(nodes[id].td);
+    mparent.push_back(nodes[id].parent < 0 ? -1 : pos[nodes[id].parent]);
+  }
+  dfs_tree_inputs[guid] = merged;
+  dfs_tree_parents[guid] = mparent;
+  return merged;
 }
 
 bool RequestManager::all_done() const {
@@ -935,7 +1031,13 @@ ffmi_status RequestManager::serve_incr_decoding(ffmi_model *llm) {
 // request_manager.cc:3083-3173
 ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   if (!llm) return FFMI_ERR_INVALID;
-  if (ssm_models.size() != 1) return FFMI_ERR_UNSUPPORTED;
+  if (ssm_models.empty()) return FFMI_ERR_INVALID;
+  // the reference asserts one SSM (merge_dfs_trees :2823-2827)
+  if (ssm_models.size() > 1 && !(spec_extensions & FFMI_SPEC_EXT_MULTI_SSM)) {
+    ffmi_set_last_error("SpecInfer with more than one SSM needs FFMI_SPEC_EXT_MULTI_SSM",
+                        __FILE__, __LINE__);
+    return FFMI_ERR_UNSUPPORTED;
+  }
   apply_limits();
   stats = Stats();
   const double t0 = now_us();
@@ -947,6 +1049,9 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   while (!all_done()) {
     ssm_prompt_behind = false;
     beam_vec->assign(ssm_models.size(), prepare_next_batch_init(*tree_bc, *tree_ir, 0));
+    // each SSM builds its own beam tree (the reference hands every SSM the
+    // init batch of model 0, :3147-3150, so all would write beam_trees[0])
+    for (size_t s = 0; s < beam_vec->size(); ++s) (*beam_vec)[s].model_id = (int)s;
     if (ssm_prompt_behind) {
       ffmi_set_last_error(
           "SpecInfer: the SSM loaded less of a prompt than the LLM (prompt longer than one "

@@ -66,6 +66,14 @@ class RequestManager {
     return max_tokens_per_batch + max_spec_tree_token_num * max_requests_per_batch;
   }
   bool push_spec_infer_tree_width(int w);
+  // Flagged extensions beyond what the reference runs (include/ffmi.h
+  // FFMI_SPEC_EXT_*): tree width / branches up to 4 per layer, and more than
+  // one SSM with their trees merged (merge_dfs_trees).  Set before widths are
+  // pushed.
+  void set_spec_extensions(int flags) { spec_extensions = flags; }
+  int get_spec_extensions() const { return spec_extensions; }
+  int max_beam_width() const;
+  int max_tree_branches() const;
   void register_tokenizer(int bos, const std::vector<int> &eos) {
     bos_token_id = bos;
     eos_token_ids = eos;
@@ -122,6 +130,12 @@ class RequestManager {
   std::vector<TokenDepth> traverse_verify_tree(size_t guid,
                                                const std::vector<TokenDepth> &input,
                                                const std::vector<TokenDepth> &output);
+  // parent index of every node of a layer-order serialised beam tree (layer
+  // d's nodes are equal groups, group j the children of node j of layer d-1)
+  static std::vector<int> layer_order_parents(const std::vector<TokenDepth> &tree);
+  // the verify step's key-major bitmask of a tree given by parent indices:
+  // mask[k] bit q <=> node k is node q or one of its ancestors
+  static void tree_bitmask(const std::vector<int> &parent, int n, BatchConfig::BitMask &m);
 
   ffmi_status serve_incr_decoding(ffmi_model *llm);
   ffmi_status serve_spec_infer(ffmi_model *llm);
@@ -170,6 +184,9 @@ class RequestManager {
   std::map<RequestGuid, GenerationResult> request_generation_results;
   RequestGuid next_available_guid = 1000000;
   std::unordered_map<RequestGuid, std::vector<TokenDepth>> dfs_tree_inputs;
+  // parent index of each node of dfs_tree_inputs[guid] (-1 for the root)
+  std::unordered_map<RequestGuid, std::vector<int>> dfs_tree_parents;
+  int spec_extensions = 0;
   std::unordered_map<RequestGuid, std::vector<std::pair<int, int>>> committed_tokens;
   std::vector<ffmi_model *> ssm_models;
   std::map<RequestGuid, ProfileInfo> profiling_requests;

@@ -33,6 +33,8 @@ F16, F32, I32 = 0, 1, 2
 # synthetic weight inits (ffmi_model_opts.weight_init) and fault kinds
 WEIGHT_INITS = {"uniform": 0, "depth_scaled": 1, "token_chain": 2}
 FAULT_NONE, FAULT_ROPE_POS = 0, 1
+# flagged SpecInfer extensions (include/ffmi.h FFMI_SPEC_EXT_*)
+SPEC_EXT_WIDTH4, SPEC_EXT_MULTI_SSM = 1, 2
 ATTN_QTILE = 32
 MAX_TREE = 64
 
@@ -98,7 +100,7 @@ class RMConfig(ctypes.Structure):
                 ("max_spec_tree_token_num", c_int), ("max_sequence_length", c_int),
                 ("bos_token_id", c_int), ("eos_token_ids", ctypes.POINTER(c_int)),
                 ("num_eos", c_int), ("spec_tree_width", ctypes.POINTER(c_int)),
-                ("num_tree_width", c_int), ("verbose", c_int)]
+                ("num_tree_width", c_int), ("verbose", c_int), ("spec_extensions", c_int)]
 
 
 class Profile(ctypes.Structure):

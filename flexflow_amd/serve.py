@@ -166,12 +166,6 @@ class Comm:
     def status(self) -> None:
         F.check(F.lib().ffmi_comm_peer_status(self.handle), "peer status")
 
-    def debug_fault(self, kind: int, layer: int = 0, arg: int = 0):
-        """Negative-control fault injection (tests only): F.FAULT_ROPE_POS
-        makes `layer`'s RoPE rotate positions >= arg as position + 1;
-        F.FAULT_NONE clears every fault (include/ffmi.h)."""
-        F.check(F.lib().ffmi_model_debug_fault(self.handle, kind, layer, arg), "debug_fault")
-
     def close(self):
         if getattr(self, "handle", None):
             F.lib().ffmi_comm_destroy(self.handle)
@@ -193,12 +187,15 @@ class GenerationResult:
 class RequestManager:
     def __init__(self, max_requests_per_batch=8, max_tokens_per_batch=128,
                  max_spec_tree_token_num=23, max_sequence_length=512, bos_token_id=1,
-                 eos_token_ids=(), spec_tree_width=(), verbose=False):
+                 eos_token_ids=(), spec_tree_width=(), verbose=False, spec_extensions=0):
+        """spec_extensions: F.SPEC_EXT_WIDTH4 (tree widths / branches up to 4;
+        the reference allows 3) | F.SPEC_EXT_MULTI_SSM (several SSMs, trees
+        merged); 0 keeps the reference's limits (include/ffmi.h)."""
         self._eos = F.int_array(list(eos_token_ids))
         self._widths = F.int_array(list(spec_tree_width))
         cfg = F.RMConfig(max_requests_per_batch, max_tokens_per_batch, max_spec_tree_token_num,
                          max_sequence_length, bos_token_id, self._eos, len(eos_token_ids),
-                         self._widths, len(spec_tree_width), int(verbose))
+                         self._widths, len(spec_tree_width), int(verbose), int(spec_extensions))
         h = ctypes.c_void_p()
         F.check(F.lib().ffmi_rm_create(ctypes.byref(cfg), ctypes.byref(h)), "rm create")
         self.handle = h
@@ -208,12 +205,6 @@ class RequestManager:
         self.max_sequence_length = max_sequence_length
         self.tokenizer = None
         self._add_special = {}
-
-    def debug_fault(self, kind: int, layer: int = 0, arg: int = 0):
-        """Negative-control fault injection (tests only): F.FAULT_ROPE_POS
-        makes `layer`'s RoPE rotate positions >= arg as position + 1;
-        F.FAULT_NONE clears every fault (include/ffmi.h)."""
-        F.check(F.lib().ffmi_model_debug_fault(self.handle, kind, layer, arg), "debug_fault")
 
     def close(self):
         if getattr(self, "handle", None):

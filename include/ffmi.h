@@ -449,7 +449,20 @@ typedef struct {
   const int *spec_tree_width; /* push_spec_infer_tree_width sequence         */
   int num_tree_width;
   int verbose;
+  int spec_extensions;     /* FFMI_SPEC_EXT_* bits (ABI 0.3); 0: the reference's limits */
 } ffmi_rm_config;
+/* Flagged SpecInfer extensions beyond what the reference runs (BASELINE
+ * configs C "tree width=4" and E "4x SSMs"):
+ *   FFMI_SPEC_EXT_WIDTH4: tree widths and branches per layer up to 4 (the
+ *     reference's MAX_BEAM_WIDTH / MAX_SPECULATIVE_TREE_BRANCHES are 3,
+ *     batch_config.h:196,200, request_manager.cc:168-171); size
+ *     max_spec_tree_token_num for the tree (27 tokens for widths (1,1,4));
+ *   FFMI_SPEC_EXT_MULTI_SSM: more than one registered SSM; their token trees
+ *     are united by path (merge_dfs_trees, request_manager.cc:2817-2878, whose
+ *     reference form asserts a single SSM) and cut to max_spec_tree_token_num
+ *     (<= 64) nodes in layer order. */
+#define FFMI_SPEC_EXT_WIDTH4 1
+#define FFMI_SPEC_EXT_MULTI_SSM 2
 
 ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out);
 void ffmi_rm_destroy(ffmi_rm *rm);
@@ -532,8 +545,9 @@ long ffmi_debug_markers(long long *dst, long n);
 const char *ffmi_status_str(ffmi_status s);
 /* message + file:line of the last failing check on this process */
 const char *ffmi_last_error(void);
-/* "ffmi 0.2 (gfx950)": 0.2 appended full_precision to ffmi_attn_cfg and
- * ffmi_model_opts (struct sizes changed) and added the *_f32 entry points */
+/* "ffmi 0.3 (gfx950)": 0.2 appended full_precision to ffmi_attn_cfg and
+ * ffmi_model_opts (struct sizes changed) and added the *_f32 entry points;
+ * 0.3 appended spec_extensions to ffmi_rm_config */
 const char *ffmi_version(void);
 
 #ifdef __cplusplus

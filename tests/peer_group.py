@@ -19,7 +19,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def _child(rank, n, conn, task, args, env, max_bytes, device):
     try:
-        os.environ.update(env)
+        for k, v in env.items():  # None: leave the variable unset (HIP's default)
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
         sys.path.insert(0, ROOT)
         sys.path.insert(0, os.path.join(ROOT, "tests"))
         import flexflow_amd as fa
@@ -50,7 +54,9 @@ def run_group(n, task, args=(), env=None, max_bytes=1 << 22, timeout=240, device
     slices of the peers it spins on (8 ranks of the 7B bench: 370 s per
     generate; with one queue per rank 7.6 s).  One queue serialises a rank's
     two streams in issue order -- the cross-stream waits still hold, only the
-    overlap is gone -- which changes no value."""
+    overlap is gone -- which changes no value.  env={"GPU_MAX_HW_QUEUES": None}
+    keeps HIP's default (up to 4 queues per rank: compute and all-reduce streams
+    overlap, the production setting of a one-process-per-GPU node)."""
     env = {"GPU_MAX_HW_QUEUES": "1", **(env or {})}
     ctx = mp.get_context("spawn")
     pipes, procs = [], []

@@ -89,14 +89,21 @@ def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
                                max_tie_frac=0.1)
 
 
-def test_peer_tp2_spec_infer_equals_incr():
+@pytest.mark.parametrize("queues", ["1", None], ids=["one_queue", "hip_default_queues"])
+def test_peer_tp2_spec_infer_equals_incr(queues):
     """SpecInfer over the transport: identical to incremental decoding of the
-    same sharded model (the reference invariant, cpp_inference_tests.sh:183-189)."""
+    same sharded model (the reference invariant, cpp_inference_tests.sh:183-189).
+    Also run with HIP's default hardware queues per rank, where the compute and
+    all-reduce streams really overlap, so a missing cross-stream event wait
+    shows up (one queue per rank serialises the two streams)."""
     from test_gpu_e2e import SSM_CFG, prompts
     ps = prompts(3, CFG4V["vocab_size"], 5, 30, 9)
     ssm = dict(SSM_CFG, vocab_size=1024)
-    inc = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, False, ssm), max_bytes=1 << 20)
-    spec = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, True, ssm), max_bytes=1 << 20)
+    env = {"GPU_MAX_HW_QUEUES": queues}
+    inc = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, False, ssm), env=env,
+                    max_bytes=1 << 20)
+    spec = run_group(2, PT.model_task, (CFG4V, 11, ps, 60, True, ssm), env=env,
+                     max_bytes=1 << 20)
     assert spec[0] == spec[1] == inc[0] == inc[1]
 
 

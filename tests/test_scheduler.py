@@ -56,14 +56,18 @@ def run_incr(ps, max_length, batch=4, max_tokens=16, eos=()):
     return res, rm.stats()
 
 
-def run_spec(ps, max_length, batch=4, max_tokens=64, widths=(1, 1, 3), disagree=0):
+def run_spec(ps, max_length, batch=4, max_tokens=64, widths=(1, 1, 3), disagree=0,
+             tree_tokens=23, ssms=None, ext=0):
+    """ssms: [(salt, disagree_pct)] per SSM (default one SSM, salt 1234)."""
     rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
                            max_sequence_length=128, spec_tree_width=widths,
-                           max_spec_tree_token_num=23)
-    llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=128, max_tree_tokens=23)
-    ssm = fa.HashModel(V, "beam", max_requests=batch, max_seq_len=128, max_tree_tokens=23,
-                       salt=1234, disagree_pct=disagree)
-    rm.register_ssm_model(ssm)
+                           max_spec_tree_token_num=tree_tokens, spec_extensions=ext)
+    llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=128,
+                       max_tree_tokens=tree_tokens)
+    for salt, dis in ssms or [(1234, disagree)]:
+        rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=batch, max_seq_len=128,
+                                           max_tree_tokens=tree_tokens, salt=salt,
+                                           disagree_pct=dis))
     res = fa.generate(rm, llm, ps, max_length=max_length)
     return res, rm.stats()
 
@@ -180,3 +184,67 @@ def test_tree_width_limit():
         fa.RequestManager(spec_tree_width=(4,))  # MAX_BEAM_WIDTH = 3 (request_manager.cc:168)
     with pytest.raises(fa.ffmi.FFMIError):
         fa.RequestManager(spec_tree_width=(2, 2))  # 4 nodes/layer > 3 (request_manager.cc:1685)
+    # the flagged width-4 extension (BASELINE config C): widths and branches <= 4
+    W4 = fa.ffmi.SPEC_EXT_WIDTH4
+    for w in [(4,), (1, 1, 4), (2, 2), (1, 4, 1)]:
+        fa.RequestManager(spec_tree_width=w, spec_extensions=W4)
+    for w in [(5,), (2, 3), (4, 2)]:
+        with pytest.raises(fa.ffmi.FFMIError):
+            fa.RequestManager(spec_tree_width=w, spec_extensions=W4)
+    with pytest.raises(fa.ffmi.FFMIError):
+        fa.RequestManager(spec_extensions=8)  # unknown extension bit
+
+
+W4 = fa.ffmi.SPEC_EXT_WIDTH4
+MULTI = fa.ffmi.SPEC_EXT_MULTI_SSM
+
+
+@pytest.mark.parametrize("disagree", [0, 30, 100])
+@pytest.mark.parametrize("widths", [(1, 1, 4), (4,), (2, 2), (1, 4), (2, 1, 2)])
+def test_spec_infer_width4_equals_incr(disagree, widths):
+    """Config C as BASELINE states it (tree width 4): SpecInfer reproduces
+    incremental decoding exactly, including trees that branch twice ((2, 2):
+    the parent-link verify walk)."""
+    ps = prompts(6, V, seed=11)
+    res, st = run_spec(ps, 90, widths=widths, disagree=disagree, tree_tokens=40, ext=W4)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 90, V), (disagree, widths)
+    assert st.llm_steps > 0
+
+
+@pytest.mark.parametrize("widths", [(1, 1, 3), (1, 1, 4)])
+@pytest.mark.parametrize("ssms", [
+    [(1234, 0), (99, 0)],                      # two agreeing SSMs: identical trees
+    [(1234, 30), (99, 30)],                    # partly different trees
+    [(1234, 30), (99, 60), (7, 90), (5, 100)],  # config E: 4 SSMs, merged up to the cap
+    [(1, 100), (2, 100), (3, 100), (4, 100)],
+])
+def test_spec_infer_multi_ssm_equals_incr(widths, ssms):
+    """Config E's 4x SSMs: the merged token tree (merge_dfs_trees restated
+    with path identity) verifies to exactly the incremental-decoding tokens;
+    merged trees beyond max_spec_tree_token_num (64) are cut in layer order."""
+    ps = prompts(6, V, seed=13)
+    res, st = run_spec(ps, 90, widths=widths, tree_tokens=64, ssms=ssms, ext=W4 | MULTI,
+                       max_tokens=64)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 90, V), (widths, ssms)
+    assert st.ssm_steps > 0 and st.llm_steps > 0
+
+
+def test_multi_ssm_merge_keeps_the_agreeing_branch():
+    """A perfect SSM merged with SSMs that never agree: the union still holds
+    the perfect chain, so every verify accepts it (as many LLM steps as the
+    perfect SSM alone), whatever the SSM order."""
+    ps = prompts(4, V, seed=7)
+    _, alone = run_spec(ps, 100, disagree=0, tree_tokens=64, ext=MULTI)
+    for ssms in ([(1234, 0), (5, 100), (6, 100)], [(5, 100), (6, 100), (1234, 0)]):
+        res, st = run_spec(ps, 100, tree_tokens=64, ssms=ssms, ext=MULTI)
+        for p, r in zip(ps, res):
+            assert r.output_tokens == expected(p, 100, V)
+        assert st.llm_steps == alone.llm_steps
+        assert st.ssm_steps == 3 * alone.ssm_steps
+
+
+def test_multi_ssm_needs_the_extension_flag():
+    with pytest.raises(fa.ffmi.FFMIError, match="UNSUPPORTED|unsupported"):
+        run_spec(prompts(2, V), 40, ssms=[(1, 0), (2, 0)])
