@@ -37,6 +37,7 @@ import flexflow_amd.ffmi as F
 import oracle_lib as O
 from hip_util import report, ulp_diff
 from parity_rules import classify, picks
+from spec_configs import SPEC, spec_setup
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from bench import LLAMA_68M, LLAMA_7B, make_prompts  # noqa: E402
@@ -46,7 +47,8 @@ pytestmark = [pytest.mark.gpu, pytest.mark.timeout(900)]
 B, P, NEW, MTB, TREE = 8, 128, 64, 1024, 23
 SEED, SSM_SEED = 20250117, 68  # bench.py's seeds
 MAX_SEQ = 512  # bench.py: max(512, prefill + decode + 1)
-SPARE = B  # oracle KV slot for the reordered (noise) runs
+SPARE = B  # oracle KV slot for fresh runs
+ALT0 = B + 1  # oracle KV slots B+1.. : request i's prompt under the reordered dot
 PER_OP_REQS = (0, 7)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -69,7 +71,7 @@ def rm_kw():
 @pytest.fixture(scope="module")
 def oracle():
     t = time.time()
-    m = O.Model(LLAMA_7B, SEED, fp16=1, max_requests=B + 1, max_seq=P + NEW + 8)
+    m = O.Model(LLAMA_7B, SEED, fp16=1, max_requests=2 * B + 1, max_seq=P + NEW + 8)
     progress(f"oracle LLaMA-7B built in {time.time() - t:.1f}s ({O.lib().orc_num_threads()} "
              "threads)")
     return m
@@ -105,19 +107,21 @@ def gpu():
     out["incr"] = [r.output_tokens for r in
                    fa.generate(fa.RequestManager(**rm_kw()), llm, ps, max_length=P + NEW)]
     llm.close()
-    vt = MTB + TREE * B
-    tree = fa.Model(LLAMA_7B, "tree", max_requests=B, max_tokens=vt, max_seq_len=MAX_SEQ,
-                    max_tree_tokens=TREE, weight_seed=SEED)
-    ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=vt, max_seq_len=MAX_SEQ,
-                   max_tree_tokens=TREE, weight_seed=SSM_SEED)
-    rm = fa.RequestManager(spec_tree_width=(1, 1, 3), **rm_kw())
-    rm.register_ssm_model(ssm)
-    out["spec"] = [r.output_tokens for r in fa.generate(rm, tree, ps, max_length=P + NEW,
-                                                        spec=True)]
-    out["spec_llm_steps"] = rm.stats().llm_steps
-    tree.close()
-    ssm.close()
-    progress("GPU incr + spec runs done")
+    # SpecInfer: widths (1,1,3) (the bench's), tree width 4, 4 SSMs
+    # (tests/spec_configs.py)
+    for name in SPEC:
+        rm, ssms, vt, tt = spec_setup(name, LLAMA_68M, B, MTB, MAX_SEQ)
+        tree = fa.Model(LLAMA_7B, "tree", max_requests=B, max_tokens=vt, max_seq_len=MAX_SEQ,
+                        max_tree_tokens=tt, weight_seed=SEED)
+        out["spec", name] = [r.output_tokens for r in fa.generate(rm, tree, ps,
+                                                                  max_length=P + NEW, spec=True)]
+        st = rm.stats()
+        out["spec_llm_steps", name] = st.llm_steps
+        out["spec_tree_tokens", name] = st.tree_tokens_verified / max(1, st.request_verifies)
+        tree.close()
+        for m in ssms:
+            m.close()
+        progress(f"GPU spec {name} done")
     return out
 
 
@@ -135,6 +139,7 @@ class Teacher:
     def __init__(self, oracle):
         self.o = oracle
         self.prompt_last = {}
+        self.alt_last = {}
 
     def logits(self, i, seq):
         """oracle logits predicting seq[P:] (rows [NEW][V])"""
@@ -143,6 +148,19 @@ class Teacher:
         cont = self.o.forward(i, np.array(seq[P:-1], np.int32), P)
         return np.vstack([self.prompt_last[i][None], cont])
 
+    def alt_logits(self, i, seq):
+        """the same rows with the oracle's dots reordered (the noise run); the
+        prompt's reordered KV stays cached in slot ALT0 + i (the oracle is
+        T-invariant: prefix + continuation == one forward)"""
+        O.set_dot_variant(1)
+        try:
+            if i not in self.alt_last:
+                self.alt_last[i] = self.o.forward(ALT0 + i, np.array(seq[:P], np.int32), 0)[-1]
+            cont = self.o.forward(ALT0 + i, np.array(seq[P:-1], np.int32), P)
+        finally:
+            O.set_dot_variant(0)
+        return np.vstack([self.alt_last[i][None], cont])
+
     def check(self, i, seq):
         lg = self.logits(i, seq)
         gen = np.array(seq[P:])
@@ -150,11 +168,7 @@ class Teacher:
         miss = np.nonzero(ids != gen)[0]
         verdicts = []
         if len(miss):
-            O.set_dot_variant(1)
-            try:
-                lg1 = self.o.forward(SPARE, np.array(seq[:-1], np.int32), 0)[P - 1:]
-            finally:
-                O.set_dot_variant(0)
+            lg1 = self.alt_logits(i, seq)
             for t in miss:
                 v = classify(lg[t], lg1[t], gen[t], ids[t])
                 v["pos"] = int(t)
@@ -181,12 +195,15 @@ def test_bench_workload_incr_decoding_vs_oracle(teacher, gpu):
     assert all(v["tie"] for v in verdicts), [v for v in verdicts if not v["tie"]]
 
 
-def test_bench_workload_spec_infer_vs_incr_and_oracle(teacher, gpu):
+@pytest.mark.parametrize("spec", list(SPEC))
+def test_bench_workload_spec_infer_vs_incr_and_oracle(teacher, gpu, spec):
     """Config C at the bench's size: SpecInfer with the 68M SSM, T = 168
-    verify steps; identical to incr decoding or oracle-checked by the rule."""
+    verify steps (widths (1,1,3)); with tree width 4 (T = 216) and with
+    config E's 4 SSMs (merged trees up to 64 tokens per request); identical to
+    incr decoding or oracle-checked by the rule."""
     tf = teacher
     same, firsts, verdicts = 0, [], []
-    for i, (a, b) in enumerate(zip(gpu["incr"], gpu["spec"])):
+    for i, (a, b) in enumerate(zip(gpu["incr"], gpu["spec", spec])):
         assert len(a) == len(b) == P + NEW
         if a == b:
             same += 1
@@ -195,9 +212,10 @@ def test_bench_workload_spec_infer_vs_incr_and_oracle(teacher, gpu):
         firsts.append(first)
         verdicts += v
         progress(f"spec request {i} differs from incr: first oracle mismatch {first}/{n}, {v}")
-    report("bench_workload_spec_b8_p128_n64", spec_equals_incr=same, requests=B,
+    report(f"bench_workload_spec_b8_p128_n64_{spec}", spec_equals_incr=same, requests=B,
            free_run_agree_of_differing=firsts, mismatches=verdicts,
-           llm_steps=gpu["spec_llm_steps"])
+           llm_steps=gpu["spec_llm_steps", spec],
+           tree_tokens_per_request_verify=gpu["spec_tree_tokens", spec])
     assert all(v["tie"] for v in verdicts), [v for v in verdicts if not v["tie"]]
 
 

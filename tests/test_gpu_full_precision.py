@@ -25,6 +25,7 @@ import oracle_lib as O
 import peer_tasks as PT
 from hip_util import Buf, report
 from peer_group import run_group
+from spec_configs import SPEC, spec_setup
 
 pytestmark = pytest.mark.gpu
 
@@ -160,16 +161,15 @@ def compare(gpu, ref, rows, n_prompts):
 
 
 def run(cfg, ps, max_length, spec, B, mtb=256, seq=256):
+    """spec: False (incr decoding), True / a tests/spec_configs.py name"""
     kw = dict(max_requests=B, max_seq_len=seq, full_precision=True)
     if spec:
-        llm = fa.Model(cfg, "tree", max_tokens=mtb + 23 * B, weight_seed=SEED, **kw)
-        ssm = fa.Model(LLAMA_68M, "beam", max_tokens=mtb + 23 * B, max_tree_tokens=23,
-                       weight_seed=68, **kw)
-        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
-                               max_sequence_length=seq, spec_tree_width=(1, 1, 3))
-        rm.register_ssm_model(ssm)
+        rm, ssms, vt, tt = spec_setup("w113" if spec is True else spec, LLAMA_68M, B, mtb, seq,
+                                      full_precision=True)
+        llm = fa.Model(cfg, "tree", max_tokens=vt, max_tree_tokens=tt, weight_seed=SEED, **kw)
         res = fa.generate(rm, llm, ps, max_length=max_length, spec=True)
-        ssm.close()
+        for m in ssms:
+            m.close()
     else:
         llm = fa.Model(cfg, "inc", max_tokens=mtb, weight_seed=SEED, **kw)
         rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
@@ -216,7 +216,9 @@ def bench_7b():
     NEW = 40
     max_length = max(n_prompts) + NEW
     incr, incr_steps = run(LLAMA_7B, ps, max_length, False, 8)
-    spec, spec_steps = run(LLAMA_7B, ps, max_length, True, 8)
+    spec, spec_steps = {}, {}
+    for name in SPEC:  # (1,1,3), tree width 4, 4 SSMs
+        spec[name], spec_steps[name] = run(LLAMA_7B, ps, max_length, name, 8)
     om = O.Model(LLAMA_7B, SEED, fp16=0, max_requests=8, max_seq=2 * max_length)
     # every request continues to max_length: the oracle runs the longest
     # continuation for all and the comparison uses each sequence's length
@@ -236,14 +238,16 @@ def test_full_precision_7b_incr_equals_oracle(bench_7b):
     assert same + len(div) == len(b["ps"])
 
 
-def test_full_precision_7b_spec_equals_incr(bench_7b):
-    """SpecInfer == incremental decoding (cpp_inference_tests.sh:183-189)"""
+@pytest.mark.parametrize("spec", list(SPEC))
+def test_full_precision_7b_spec_equals_incr(bench_7b, spec):
+    """SpecInfer == incremental decoding (cpp_inference_tests.sh:183-189), with
+    widths (1,1,3), tree width 4 and 4 SSMs"""
     b = bench_7b
-    same = sum(a == c for a, c in zip(b["spec"], b["incr"]))
-    report("full_precision_7b_32L_spec_vs_incr", identical=same, requests=len(b["ps"]),
-           incr_steps=b["incr_steps"], spec_steps=b["spec_steps"])
+    same = sum(a == c for a, c in zip(b["spec"][spec], b["incr"]))
+    report(f"full_precision_7b_32L_spec_vs_incr_{spec}", identical=same, requests=len(b["ps"]),
+           incr_steps=b["incr_steps"], spec_steps=b["spec_steps"][spec])
     if same < len(b["ps"]):  # only at an fp32 tie of the oracle's row
-        compare(b["spec"], b["ref"], b["rows"], b["n_prompts"])
+        compare(b["spec"][spec], b["ref"], b["rows"], b["n_prompts"])
 
 
 def test_full_precision_tp8_processes_equal_tp1():
@@ -264,3 +268,40 @@ def test_full_precision_tp8_processes_equal_tp1():
     report("full_precision_7b_tp8_vs_tp1", requests=len(ps), **same)
     assert out[False][0] == out[False][1], same
     assert out[True][0] == out[True][1], same
+
+
+def test_full_precision_negative_control_rope_fault():
+    """The literal fp32 bars must FAIL a real bug: 4 layers at LLaMA-7B widths,
+    4 prompts, 16 new tokens.  Clean: every token equals the fp32 oracle's
+    greedy decode.  Layer 2's RoPE one position off for decode tokens
+    (ffmi_model_debug_fault FFMI_FAULT_ROPE_POS on the DT_FLOAT handles): at
+    least one request must leave the oracle's sequence at a pick whose oracle
+    logit gap is far beyond an fp32 tie (FP32_TIE)."""
+    cfg = dict(LLAMA_7B, num_layers=4)
+    ps = prompts(4, 16, 17, 31)
+    n_prompt = 17  # with BOS
+    NEW = 16
+    m = fa.Model(cfg, "inc", max_requests=4, max_tokens=256, max_seq_len=128, weight_seed=SEED,
+                 full_precision=True)
+    runs = {}
+    for fault in (False, True):
+        m.debug_fault(F.FAULT_ROPE_POS if fault else F.FAULT_NONE, 2, n_prompt)
+        res = fa.generate(fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=256,
+                                            max_sequence_length=128), m, ps,
+                          max_length=n_prompt + NEW)
+        runs[fault] = [r.output_tokens for r in res]
+    m.debug_fault(F.FAULT_NONE)
+    m.close()
+    om = O.Model(cfg, SEED, fp16=0, max_requests=4, max_seq=128)
+    ref, rows = oracle_greedy(om, [[1] + p for p in ps], NEW)
+    same, div = compare(runs[False], ref, rows, [n_prompt] * 4)
+    gaps = []
+    for b, (g, r) in enumerate(zip(runs[True], ref)):
+        if list(g) != list(r):
+            t = next(i for i in range(len(g)) if g[i] != r[i])
+            row = rows[b][t - n_prompt]
+            gaps.append(float(row[r[t]] - row[g[t]]))
+    report("full_precision_negative_control_rope_layer2", clean_identical=same,
+           clean_divergences=div, faulted_divergence_gaps=gaps)
+    assert same == 4, div
+    assert gaps and max(gaps) > 100 * FP32_TIE, ("fault NOT detected", gaps)

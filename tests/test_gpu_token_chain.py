@@ -43,6 +43,7 @@ import flexflow_amd as fa
 import oracle_lib as O
 from hip_util import report
 from parity_rules import picks
+from spec_configs import SPEC, spec_setup
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
 
@@ -78,28 +79,31 @@ def runs():
     out["incr"] = [r.output_tokens for r in fa.generate(rmi, llm, ps, max_new_tokens=NEW + 1)]
     out["incr_steps"] = rmi.stats().llm_steps
     llm.close()
-    vt = 128 + 23 * B
-    tree = fa.Model(LLAMA_7B, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
-                    max_tree_tokens=23, weight_seed=SEED, weight_init="token_chain")
-    ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=vt, max_seq_len=128,
-                   max_tree_tokens=23, weight_seed=SSM_SEED, weight_init="token_chain")
-    rm = fa.RequestManager(spec_tree_width=(1, 1, 3), max_spec_tree_token_num=23, **kw)
-    rm.register_ssm_model(ssm)
-    out["spec"] = [r.output_tokens for r in fa.generate(rm, tree, ps, max_new_tokens=NEW + 1,
-                                                        spec=True)]
-    st = rm.stats()
-    out["spec_steps"] = st.llm_steps
-    out["spec_committed"] = st.tokens_committed
-    out["spec_request_verifies"] = st.request_verifies
-    tree.close()
-    ssm.close()
-    progress(f"GPU runs done: incr steps {out['incr_steps']}, spec steps {out['spec_steps']}")
+    # SpecInfer: config C as the reference runs it (1,1,3), with tree width 4
+    # (1,1,4), and config E's 4 SSMs (tests/spec_configs.py)
+    for name in SPEC:
+        rm, ssms, vt, tt = spec_setup(name, LLAMA_68M, B, 128, 128, weight_init="token_chain")
+        tree = fa.Model(LLAMA_7B, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
+                        max_tree_tokens=tt, weight_seed=SEED, weight_init="token_chain")
+        out["spec", name] = [r.output_tokens for r in
+                             fa.generate(rm, tree, ps, max_new_tokens=NEW + 1, spec=True)]
+        st = rm.stats()
+        out["spec_steps", name] = st.llm_steps
+        out["spec_committed", name] = st.tokens_committed
+        out["spec_request_verifies", name] = st.request_verifies
+        out["spec_tree_tokens", name] = st.tree_tokens_verified
+        tree.close()
+        for m in ssms:
+            m.close()
+        progress(f"GPU {name} done: incr steps {out['incr_steps']}, spec steps "
+                 f"{out['spec_steps', name]}")
     return out
 
 
-def test_token_chain_full_depth_literal_bars(runs):
-    """LLaMA-7B (32 layers) and the 68M SSM in the token-chain init, batch 8:
-    the reference's literal bars, every request."""
+@pytest.fixture(scope="module")
+def incr_check(runs):
+    """incr decoding's tokens against the oracle: first divergence per request
+    and the smallest top-2 logit margin"""
     t = time.time()
     orc = O.Model(LLAMA_7B, SEED, fp16=1, max_requests=1, max_seq=NEW + 32, weight_init=2)
     progress(f"oracle built in {time.time() - t:.1f}s")
@@ -117,14 +121,26 @@ def test_token_chain_full_depth_literal_bars(runs):
         margins.append(float((srt[:, -1] - srt[:, -2]).min()))
         # the chain: every pick is perm^-1 of the token before it
         assert all(gen[i] == inv[seq[n_prompt - 1 + i]] for i in range(NEW))
-    same = sum(a == b for a, b in zip(runs["incr"], runs["spec"]))
-    acc = runs["spec_committed"] / max(1, runs["spec_request_verifies"])
-    report("token_chain_7b_32L_b8", free_run_agree=agree, min_top2_margin=min(margins),
+    return agree, margins
+
+
+@pytest.mark.parametrize("spec", list(SPEC))
+def test_token_chain_full_depth_literal_bars(runs, incr_check, spec):
+    """LLaMA-7B (32 layers) and the 68M SSM(s) in the token-chain init, batch 8:
+    the reference's literal bars, every request, for SpecInfer with widths
+    (1,1,3), with tree width 4 and with 4 SSMs."""
+    agree, margins = incr_check
+    same = sum(a == b for a, b in zip(runs["incr"], runs["spec", spec]))
+    acc = runs["spec_committed", spec] / max(1, runs["spec_request_verifies", spec])
+    tree_tok = runs["spec_tree_tokens", spec] / max(1, runs["spec_request_verifies", spec])
+    report(f"token_chain_7b_32L_b8_{spec}", free_run_agree=agree, min_top2_margin=min(margins),
            spec_equals_incr=same, requests=B, incr_llm_steps=runs["incr_steps"],
-           spec_llm_steps=runs["spec_steps"], tokens_per_request_verify=acc)
-    progress(f"agree {agree}, spec==incr {same}/{B}, steps {runs['incr_steps']} vs "
-             f"{runs['spec_steps']}, acceptance {acc:.2f}")
+           spec_llm_steps=runs["spec_steps", spec], tokens_per_request_verify=acc,
+           tree_tokens_per_request_verify=tree_tok, widths=SPEC[spec]["widths"],
+           ssms=len(SPEC[spec]["ssm_seeds"]))
+    progress(f"{spec}: agree {agree}, spec==incr {same}/{B}, steps {runs['incr_steps']} vs "
+             f"{runs['spec_steps', spec]}, acceptance {acc:.2f}, tree tokens {tree_tok:.1f}")
     assert all(a == NEW for a in agree), agree           # first 30 (all 40) identical
     assert same == B, (same, B)                          # SpecInfer == incr decoding
-    assert runs["incr_steps"] >= 1.5 * runs["spec_steps"], (runs["incr_steps"],
-                                                            runs["spec_steps"])
+    assert runs["incr_steps"] >= 1.5 * runs["spec_steps", spec], (
+        runs["incr_steps"], runs["spec_steps", spec])
