@@ -239,6 +239,43 @@ def cpu_baseline(acceptance=1.0, prompt_len=128, batch=8, budget_s=12.0, incr_bu
                                          f"{prompt_len}-{prompt_len + isteps - 1}, {dti:.1f}s"})
 
 
+def run_leg(llm_cfg, ssm_cfg, prompts, max_len, B, mtb, rm_kw, args, widths, tree, seeds, ext,
+            init):
+    """One SpecInfer side leg (rank 0, one GPU): a warm and a timed generate
+    of the headline's prompts with other tree widths / SSMs / weights."""
+    kw = dict(rm_kw, max_spec_tree_token_num=tree)
+    vt = mtb + tree * B
+    llm = fa.Model(llm_cfg, "tree", max_requests=B, max_tokens=vt,
+                   max_seq_len=kw["max_sequence_length"], max_tree_tokens=tree,
+                   weight_seed=20250117, weights_folder=args.llm_weights, weight_init=init)
+    ssms = [fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=vt,
+                     max_seq_len=kw["max_sequence_length"], max_tree_tokens=tree, weight_seed=sd,
+                     weights_folder=args.ssm_weights, weight_init=init) for sd in seeds]
+    rm = fa.RequestManager(spec_tree_width=widths, spec_extensions=ext, **kw)
+    for m in ssms:
+        rm.register_ssm_model(m)
+    run_generate(rm, llm, prompts, max_len, True)  # warm (graphs captured)
+    device_sync()
+    t = time.time()
+    n, lat, _ = run_generate(rm, llm, prompts, max_len, True)
+    device_sync()
+    dt = time.time() - t
+    st = rm.stats()
+    llm.close()
+    for m in ssms:
+        m.close()
+    return {"value": round(n / dt, 2), "unit": "tokens/s", "ms_per_generate": round(dt * 1e3, 1),
+            "tree_widths": list(widths), "ssms": len(seeds), "max_spec_tree_token_num": tree,
+            "weight_init": init,
+            "tokens_per_request_verify": round(st.tokens_committed / max(1, st.request_verifies), 3),
+            "tree_tokens_per_request_verify": round(st.tree_tokens_verified /
+                                                    max(1, st.request_verifies), 2),
+            "llm_steps_per_generate": st.llm_steps, "ssm_steps_per_generate": st.ssm_steps,
+            "verify_step_ms": round(st.llm_us / 1e3 / max(1, st.llm_steps), 3),
+            "ssm_step_us": round(st.ssm_us / max(1, st.ssm_steps), 1),
+            "p50_token_latency_ms": round(statistics.median(lat) / 1000.0, 3)}
+
+
 def pmc_traffic(kernel):
     """HBM bytes per launch of the roofline kernel, measured with rocprofv3
     --pmc FETCH_SIZE in a separate run (scripts/round_gpu.sh ->
@@ -325,6 +362,8 @@ def main():
     ap.add_argument("--max-tokens-per-batch", type=int, default=1024)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-incr", action="store_true", help="skip the incr-decoding side run")
+    ap.add_argument("--no-legs", action="store_true",
+                    help="skip the side legs (tree width 4, 4 SSMs, token-chain acceptance)")
     ap.add_argument("--profile", type=int, default=1, help="op profiling level in timed steps")
     ap.add_argument("--layers", type=int, default=0, help="override LLM layer count (debug)")
     ap.add_argument("--llm-weights", default=None,
@@ -578,12 +617,35 @@ def main():
                                 "p50_token_latency_ms": round(statistics.median(lat) / 1000, 3),
                                 "llm_steps": rmi.stats().llm_steps}
         inc.close()
+    if rank == 0 and world == 1 and spec and not args.no_legs:
+        # side legs, one warm + one timed generate each, same prompts and
+        # lengths as the headline (BASELINE configs C / E as stated, and
+        # SpecInfer at the acceptance a trained SSM gives):
+        #  spec_width4      widths (1,1,4), 27-token trees (FFMI_SPEC_EXT_WIDTH4)
+        #  spec_4ssm        4 LLaMA-68M SSMs (seeds 68-71), merged trees <= 64
+        #                   tokens (FFMI_SPEC_EXT_MULTI_SSM)
+        #  spec_token_chain widths (1,1,3), both models in the token-chain
+        #                   synthetic init (include/ffmi.h): the SSM predicts
+        #                   the LLM's greedy chain, so verify steps commit deep
+        #                   paths (tree_inc_multihead_self_attention.cu:335-396)
+        legs = {"spec_width4": dict(widths=(1, 1, 4), tree=27, seeds=(68,),
+                                    ext=fa.ffmi.SPEC_EXT_WIDTH4, init="uniform"),
+                "spec_4ssm": dict(widths=(1, 1, 3), tree=64, seeds=(68, 69, 70, 71),
+                                  ext=fa.ffmi.SPEC_EXT_MULTI_SSM, init="uniform"),
+                "spec_token_chain": dict(widths=(1, 1, 3), tree=23, seeds=(68,), ext=0,
+                                         init="token_chain")}
+        llm.close()  # free the headline model's 13.5 GB first
+        llm = None
+        for name, lg in legs.items():
+            out[name] = run_leg(llm_cfg, ssm_cfg, prompts, max_len, B, mtb, rm_kw, args, **lg)
+            progress(f"leg {name}: {out[name]['value']} tokens/s")
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(
             acceptance=out.get("tokens_per_request_verify", 1.0) if spec else 1.0)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    llm.close()
+    if llm is not None:
+        llm.close()
     if comm:
         comm.close()
 

@@ -204,6 +204,8 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
                           hipStream_t s, bool out_packed = false, Partials x2p = {}, const char *gather = nullptr,
                           char *blob_dst = nullptr, size_t blob_bytes = 0);
+// FFMI_FAULT_RESID_ROUND negative control (tests only; process-wide)
+void set_norm_fault(bool on);
 hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
                             uint16_t *out, int H, hipStream_t s);
 hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,

@@ -38,6 +38,9 @@ __device__ __forceinline__ T block_sum(T v, T *scratch) {
 // and waited for the x1 load before issuing the slabs -- two round trips):
 //   0: x1 only   1: x1 + x2 (fp16)   2: x1 + split-K slabs   3: gather (x1 =
 //   embedding table, rows picked by the step's token ids)
+//   4 / 5: 1 / 2 with the FFMI_FAULT_RESID_ROUND negative control (tests
+//   only): the sum of squares takes the UNROUNDED fp32 residual sum, where
+//   residual_rms_norm_kernels.cu:112-114 squares the half-rounded one
 template <int NT, int MAXC, int MAXS, int SRC>
 __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ x1, const uint16_t *__restrict__ x2,
@@ -51,13 +54,15 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   const int nchunk = H >> 3;
   // gather: x1 is the embedding table and row t reads its token's row (the
   // embedding lookup fused into the first layer's norm; res_out gets the copy)
-  const uint16_t *a = SRC == 3 ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
-                               : x1 + (size_t)row * H;
+  constexpr bool FAULT = SRC >= 4;
+  constexpr int S = FAULT ? SRC - 3 : SRC;  // the data source of the variant
+  const uint16_t *a = S == 3 ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
+                             : x1 + (size_t)row * H;
   // blob fetch: gather is the step's staging blob in mapped host memory; the
   // grid copies it into device memory for the step's later kernels (replaces
   // the H2D copy node and the system-scope boundary after it), its loads in
   // flight together with the token-id read
-  if (SRC == 3 && blob_dst) {
+  if (S == 3 && blob_dst) {
     const uint4 *src = reinterpret_cast<const uint4 *>(gather);
     for (int i = row * NT + threadIdx.x; i < blob_n16; i += T * NT) blob_dst[i] = src[i];
   }
@@ -83,7 +88,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = min((int)threadIdx.x + c * NT, nchunk - 1);  // clamped: no branch
-    if (SRC == 2) {
+    if (S == 2) {
       const float *q = x2p + (size_t)row * pNP + ch * 8;
 #pragma unroll
       for (int sl = 0; sl < MAXS; ++sl) {
@@ -92,36 +97,47 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
         shi[sl] = *reinterpret_cast<const f4 *>(qs + 4);
       }
     }
-    if (SRC == 1) xb[c] = *reinterpret_cast<const uint4 *>(x2 + (size_t)row * H + ch * 8);
+    if (S == 1) xb[c] = *reinterpret_cast<const uint4 *>(x2 + (size_t)row * H + ch * 8);
     v[c] = *reinterpret_cast<const uint4 *>(a + ch * 8);
     wv[c] = *reinterpret_cast<const uint4 *>(w + ch * 8);
-    if (SRC == 2 && MAXC > 1) xb[c] = fold();
+    if (S == 2 && MAXC > 1) xb[c] = fold();
   }
-  if (SRC == 2 && MAXC == 1) xb[0] = fold();
+  if (S == 2 && MAXC == 1) xb[0] = fold();
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * NT;
     if (ch < nchunk) {
       uint4 xa = v[c];
-      if (SRC == 1 || SRC == 2) {
+      if (S == 1 || S == 2) {
         const uint4 xbb = xb[c];
         const __half2 *pa = reinterpret_cast<const __half2 *>(&xa);
         const __half2 *pb = reinterpret_cast<const __half2 *>(&xbb);
+        if (FAULT) {  // negative control: square the unrounded sum
+          const uint16_t *ea = reinterpret_cast<const uint16_t *>(&xa);
+          const uint16_t *eb = reinterpret_cast<const uint16_t *>(&xbb);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            const float f = h2f_(ea[q]) + h2f_(eb[q]);
+            ss += f * f;
+          }
+        }
         __half2 r[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) r[q] = __hadd2(pa[q], pb[q]);  // correctly rounded
         xa = *reinterpret_cast<uint4 *>(r);
         *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
-      } else if (SRC == 3) {
+      } else if (S == 3) {
         *reinterpret_cast<uint4 *>(res_out + (size_t)row * H + ch * 8) = xa;
       }
       v[c] = xa;
       const uint16_t *e = reinterpret_cast<const uint16_t *>(&xa);
+      if (!FAULT) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        float f = h2f_(e[q]);
-        ss += f * f;
+        for (int q = 0; q < 8; ++q) {
+          float f = h2f_(e[q]);
+          ss += f * f;
+        }
       }
     }
   }
@@ -147,6 +163,11 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     }
   }
 }
+
+// FFMI_FAULT_RESID_ROUND (tests only, process-wide): residual norms take the
+// faulted variants (SRC 4 / 5)
+static bool g_norm_fault = false;
+void set_norm_fault(bool on) { g_norm_fault = on; }
 
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
@@ -195,6 +216,24 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
     else if (src == 1) FFMI_RMS3(NT, MC, 1, 1);            \
     else FFMI_RMS3(NT, MC, 1, 3);                          \
   } while (0)
+  if (g_norm_fault && (src == 1 || src == 2)) {  // negative control (tests only)
+#define FFMI_RMSF(NT)                                      \
+  do {                                                     \
+    if (src == 1) FFMI_RMS3(NT, 1, 1, 4);                  \
+    else if (ms == 1) FFMI_RMS3(NT, 1, 1, 5);              \
+    else if (ms == 2) FFMI_RMS3(NT, 1, 2, 5);              \
+    else if (ms == 4) FFMI_RMS3(NT, 1, 4, 5);              \
+    else if (ms == 8) FFMI_RMS3(NT, 1, 8, 5);              \
+    else return hipErrorInvalidValue;                      \
+  } while (0)
+    if (nchunk <= 128) FFMI_RMSF(128);
+    else if (nchunk <= 256) FFMI_RMSF(256);
+    else if (nchunk <= 512) FFMI_RMSF(512);
+    else if (nchunk <= 1024) FFMI_RMSF(1024);
+    else return hipErrorInvalidValue;
+#undef FFMI_RMSF
+    return hipGetLastError();
+  }
   if (nchunk <= 128 && ms == 12) FFMI_RMS3(128, 1, 12, 2);
   else if (nchunk <= 128 && ms == 16) FFMI_RMS3(128, 1, 16, 2);
   else if (nchunk <= 128) FFMI_RMS(128, 1);

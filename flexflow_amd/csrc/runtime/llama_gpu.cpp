@@ -297,6 +297,12 @@ struct LlamaGPU : public ffmi_model {
     // the tables are rewritten with blocking copies: finish the model's
     // (non-blocking) stream first in every branch
     if (stream) FFMI_HIP(hipStreamSynchronize(stream));
+    if (kind == FFMI_FAULT_RESID_ROUND || kind == FFMI_FAULT_NONE) {
+      // captured graphs hold the launches of the other norm variant
+      ffmi::set_norm_fault(kind == FFMI_FAULT_RESID_ROUND);
+      clear_graphs();
+      if (kind == FFMI_FAULT_RESID_ROUND) return FFMI_OK;
+    }
     if (kind == FFMI_FAULT_NONE) {
       for (auto &L : layers) {
         ffmi_status st = ffmi::attn_rope_fault(L.attn, -1);

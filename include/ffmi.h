@@ -430,9 +430,15 @@ long ffmi_model_debug_width(ffmi_model *m, int which);
  *     decode phase, apply_rotary_embedding_hf inc_multihead_self_attention.cu:
  *     664-738 with a wrong abs_depth); layer -1: every layer; arg < 0
  *     clears it.
+ *   FFMI_FAULT_RESID_ROUND (layer, arg ignored; fp16 models, process-wide):
+ *     the residual RMSNorm kernel squares the UNROUNDED fp32 residual sum
+ *     x1 + x2 where residual_rms_norm_kernels.cu:112-114 rounds it to half
+ *     first -- a rounding-point bug that moves the normalised outputs by at
+ *     most an ulp (the norms folded into the decode GEMMs are not faulted).
  *   FFMI_FAULT_NONE clears every fault. */
 #define FFMI_FAULT_NONE 0
 #define FFMI_FAULT_ROPE_POS 1
+#define FFMI_FAULT_RESID_ROUND 2
 ffmi_status ffmi_model_debug_fault(ffmi_model *m, int kind, int layer, int arg);
 /* select the HIP device of the calling thread (one process per GPU) */
 ffmi_status ffmi_set_device(int device);

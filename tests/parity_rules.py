@@ -28,13 +28,23 @@ oracle's is such a tie:
   reordering noise (test_gpu_bench_workload.py's negative control must FAIL
   this rule).  On shallow models sigma_pair is tiny and the rule reduces to
   the <= 2-ulp probability tie of test_gpu_e2e.py.
+
+Ceiling on the number of ties: a bug that moves logits by 1-3 sigma_pair at
+many positions would pass the per-position test, so every token test also
+caps the ties at max(2, TIE_MAX_FRAC of its picks) (measured at the bench
+workload: 6 / 512 incr decoding, 9 / 512 SpecInfer), or at the count the
+measured noise itself predicts where a test has it for every row
+(expected_flips: sum over rows of Phi(-gap / sigma_pair)).
 """
+import math
+
 import numpy as np
 
 from hip_util import ulp_diff
 
 TIE_ULP = 2
 TIE_SIGMA = 3.0
+TIE_MAX_FRAC = 0.03
 
 
 def p16_row(row):
@@ -63,3 +73,30 @@ def picks(logits):
     import oracle_lib as O
     ids, _ = O.softmax_argmax(np.ascontiguousarray(logits, np.float32), fp16=1)
     return ids
+
+
+def tie_budget(total):
+    """ties allowed among `total` picks"""
+    return max(2, int(math.ceil(TIE_MAX_FRAC * total)))
+
+
+def assert_ties(verdicts, total, budget=None):
+    """every mismatch a tie, and no more ties than the budget"""
+    bad = [v for v in verdicts if not v["tie"]]
+    assert not bad, bad
+    cap = tie_budget(total) if budget is None else budget
+    assert len(verdicts) <= cap, ("more ties than the budget", len(verdicts), cap, total)
+
+
+def expected_flips(z0, z1):
+    """rows z0 (reference) and z1 (the reordered run): the number of greedy
+    picks the reordering noise is expected to flip, sum over rows of
+    Phi(-gap / sigma_pair) with gap the top-2 distance of z0 and sigma_pair
+    = sqrt(2) x std(z1 - z0) of the row"""
+    z0 = np.asarray(z0, np.float64)
+    d = np.asarray(z1, np.float64) - z0
+    sig = np.sqrt(2.0) * d.std(axis=1)
+    top = np.sort(z0, axis=1)[:, -2:]
+    gap = top[:, 1] - top[:, 0]
+    x = -gap / np.maximum(sig, 1e-30)
+    return float(sum(0.5 * math.erfc(-v / math.sqrt(2.0)) for v in x))

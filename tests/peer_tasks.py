@@ -120,20 +120,18 @@ def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ss
     token j + 1 of sequence s is s's j-th row of its block."""
     B = len(prompts)
     mtb = 256
-    if spec:
-        extra = 23 * B
-        m = fa.Model(cfg, "tree", max_requests=B, max_tokens=mtb + extra, max_seq_len=128,
-                     weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm,
+    if spec:  # True or a tests/spec_configs.py name; the SSMs replicated per rank
+        from spec_configs import spec_setup
+        rm, ssms, vt, tt = spec_setup("w113" if spec is True else spec, ssm_cfg, B, mtb, 128,
+                                      weight_init=weight_init)
+        m = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
+                     max_tree_tokens=tt, weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm,
                      weight_init=weight_init)
-        ssm = fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=mtb + extra, max_seq_len=128,
-                       max_tree_tokens=23, weight_seed=68, weight_init=weight_init)
-        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
-                               max_sequence_length=128, spec_tree_width=(1, 1, 3))
-        rm.register_ssm_model(ssm)
         res = fa.generate(rm, m, prompts, max_length=max_length, spec=True)
         out = {"tokens": [r.output_tokens for r in res], "llm_steps": rm.stats().llm_steps}
         m.close()
-        ssm.close()
+        for x in ssms:
+            x.close()
         return out
     nt = B + len(tf_seqs)
     m = fa.Model(cfg, "inc", max_requests=max(B, nt), max_tokens=2 * mtb, max_seq_len=128,

@@ -36,7 +36,7 @@ import flexflow_amd as fa
 import flexflow_amd.ffmi as F
 import oracle_lib as O
 from hip_util import report, ulp_diff
-from parity_rules import classify, picks
+from parity_rules import assert_ties, classify, picks, tie_budget
 from spec_configs import SPEC, spec_setup
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -191,8 +191,8 @@ def test_bench_workload_incr_decoding_vs_oracle(teacher, gpu):
         progress(f"incr request {i}: first mismatch {first}/{n}, {v}")
     report("bench_workload_incr_b8_p128_n64", free_run_agree=firsts,
            free_run_ge_30=sum(f >= 30 for f in firsts), mismatches=verdicts,
-           exact=total - len(verdicts), total=total)
-    assert all(v["tie"] for v in verdicts), [v for v in verdicts if not v["tie"]]
+           exact=total - len(verdicts), total=total, tie_budget=tie_budget(total))
+    assert_ties(verdicts, total)
 
 
 @pytest.mark.parametrize("spec", list(SPEC))
@@ -212,11 +212,13 @@ def test_bench_workload_spec_infer_vs_incr_and_oracle(teacher, gpu, spec):
         firsts.append(first)
         verdicts += v
         progress(f"spec request {i} differs from incr: first oracle mismatch {first}/{n}, {v}")
+    total = B * NEW  # the run's picks (sequences equal to incr decoding were checked there)
     report(f"bench_workload_spec_b8_p128_n64_{spec}", spec_equals_incr=same, requests=B,
            free_run_agree_of_differing=firsts, mismatches=verdicts,
            llm_steps=gpu["spec_llm_steps", spec],
-           tree_tokens_per_request_verify=gpu["spec_tree_tokens", spec])
-    assert all(v["tie"] for v in verdicts), [v for v in verdicts if not v["tie"]]
+           tree_tokens_per_request_verify=gpu["spec_tree_tokens", spec],
+           tie_budget=tie_budget(total))
+    assert_ties(verdicts, total)
 
 
 def within(ours, ref, ulp=2):
@@ -362,5 +364,47 @@ def test_negative_control_rope_fault_is_detected(oracle):
     report("negative_control_rope_layer16", clean=out[False], faulted=out[True],
            faulted_non_ties=sum(not v["tie"] for v in out[True]))
     progress(f"negative control: clean {out[False]}, faulted {len(out[True])} mismatches")
-    assert all(v["tie"] for v in out[False]), out[False]
+    assert_ties(out[False], 4 * 24)
     assert any(not v["tie"] for v in out[True]), ("fault NOT detected", out[True])
+
+
+def test_negative_control_residual_rounding_fault_is_detected(oracle):
+    """A rounding-point bug must fail the per-op local check: the residual
+    RMSNorm kernel squaring the unrounded fp32 residual sum
+    (ffmi_model_debug_fault FFMI_FAULT_RESID_ROUND; the reference rounds it to
+    half first, residual_rms_norm_kernels.cu:112-114).  The bench model's
+    T = 1024 prefill is captured with the fault; the norms of layers 0, 15 and
+    31 (request 0's rows) are checked as test_bench_workload_prefill_T1024_per_op
+    checks them (the oracle's norm on the GPU's own captured input, bit-exact
+    demanded): at least one must NOT be bit-exact.  The shift is below an ulp
+    of most outputs (the rms moves by ~1e-5 relative), so the 2-ulp bar alone
+    would pass it -- the bit-exact norm bar is what catches it."""
+    ps = bench_prompts()
+    llm = fa.Model(LLAMA_7B, "inc", max_requests=B, max_tokens=MTB, max_seq_len=MAX_SEQ,
+                   weight_seed=SEED)
+    llm.debug_fault(F.FAULT_RESID_ROUND)
+    llm.set_debug(True)
+    fa.generate(fa.RequestManager(**rm_kw()), llm, ps, max_length=P + 1)
+    rows = np.arange(P)
+    eps = LLAMA_7B["rms_eps"]
+    res = {}
+    for l in (0, 15, 31):
+        p = f"model.layers.{l}."
+        res_in = (llm.debug_tensor("embed", 0) if l == 0 else llm.debug_tensor("hidden", l - 1))[rows]
+        g = {op: llm.debug_tensor(op, l)[rows] for op in ("attn_norm", "o_proj", "ffn_norm")}
+        loc_attn = O.rmsnorm(res_in, oracle.weight(p + "input_layernorm.weight"), eps)
+        r1 = O.round16(res_in + g["o_proj"])
+        loc_ffn = O.rmsnorm(r1, oracle.weight(p + "post_attention_layernorm.weight"), eps)
+        for name, ours, ref in (("attn_norm", g["attn_norm"], loc_attn),
+                                ("ffn_norm", g["ffn_norm"], loc_ffn)):
+            st = within(ours, ref)
+            st["rows_not_exact"] = int((ours != ref).any(axis=1).sum())
+            res[f"{name}_{l}"] = st
+    llm.debug_fault(F.FAULT_NONE)
+    llm.close()
+    report("negative_control_residual_rounding", rows=P, checks=res)
+    progress(f"residual-rounding control: {res}")
+    # (layer 0's attn_norm has no residual add: the embedding alone)
+    assert any(v["exact"] < 1.0 for k, v in res.items() if k != "attn_norm_0"), \
+        ("fault NOT detected", res)
+    assert res["attn_norm_0"]["exact"] == 1.0, res["attn_norm_0"]

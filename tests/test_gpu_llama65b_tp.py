@@ -29,6 +29,7 @@ import peer_tasks as PT
 from hip_util import report
 from parity_rules import classify, picks
 from peer_group import run_group
+from spec_configs import spec_setup
 
 pytestmark = [pytest.mark.gpu, pytest.mark.timeout(1100)]
 
@@ -46,21 +47,18 @@ def prompts():
     return [rng.integers(3, 32000, size=12).tolist() for _ in range(3)]
 
 
-def tp1_run(ps, max_length, tf_seqs, weight_init):
+def tp1_run(ps, max_length, tf_seqs, weight_init, spec_cfg):
     """TP = 1 in this process: SpecInfer, then incr decoding + the teacher-
     forced step over tf_seqs (one prefill, logits [T][V])"""
     B = len(ps)
-    tree = fa.Model(LLAMA_65B, "tree", max_requests=B, max_tokens=256 + 23 * B, max_seq_len=128,
-                    weight_seed=SEED, weight_init=weight_init)
-    ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=256 + 23 * B, max_seq_len=128,
-                   max_tree_tokens=23, weight_seed=68, weight_init=weight_init)
-    rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=256,
-                           max_sequence_length=128, spec_tree_width=(1, 1, 3))
-    rm.register_ssm_model(ssm)
+    rm, ssms, vt, tt = spec_setup(spec_cfg, LLAMA_68M, B, 256, 128, weight_init=weight_init)
+    tree = fa.Model(LLAMA_65B, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
+                    max_tree_tokens=tt, weight_seed=SEED, weight_init=weight_init)
     spec = [r.output_tokens for r in fa.generate(rm, tree, ps, max_length=max_length, spec=True)]
     spec_steps = rm.stats().llm_steps
     tree.close()
-    ssm.close()
+    for m in ssms:
+        m.close()
     nt = len(tf_seqs)
     m = fa.Model(LLAMA_65B, "inc", max_requests=max(B, nt), max_tokens=512, max_seq_len=128,
                  weight_seed=SEED, weight_init=weight_init)
@@ -93,21 +91,24 @@ def judge(seqs, n_prompts, lg1, lg8, L):
     return verdicts, exact, total
 
 
-@pytest.mark.parametrize("weight_init", ["uniform", "token_chain"])
-def test_llama65b_80L_tp8_processes_vs_tp1(weight_init):
+@pytest.mark.parametrize("weight_init,spec_cfg", [("uniform", "w113"), ("token_chain", "w113"),
+                                                  ("token_chain", "ssm4")])
+def test_llama65b_80L_tp8_processes_vs_tp1(weight_init, spec_cfg):
+    """spec_cfg: tests/spec_configs.py -- widths (1,1,3) with one SSM, or
+    config E as BASELINE states it, 4 SSMs (merged trees, up to 64 tokens)"""
     ps = prompts()
     n_prompts = [len(p) + 1 for p in ps]
     max_length = n_prompts[0] + NEW
     t0 = time.time()
     # TP = 8: SpecInfer, then incr decoding with the teacher-forced step over
     # both runs' sequences
-    spec8 = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, True, LLAMA_68M,
-                                                (), weight_init),
-                      max_bytes=(512 + 23 * 3 + 16) * 8192 * 2, timeout=900)
+    spec8 = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, spec_cfg,
+                                                LLAMA_68M, (), weight_init),
+                      max_bytes=(512 + 64 * 3 + 16) * 8192 * 2, timeout=900)
     s8spec = spec8[0]["tokens"]
     inc8 = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, False, LLAMA_68M,
                                                tuple(s8spec), weight_init),
-                     max_bytes=(512 + 23 * 3 + 16) * 8192 * 2, timeout=900)
+                     max_bytes=(512 + 64 * 3 + 16) * 8192 * 2, timeout=900)
     for r in range(TP):
         assert spec8[r]["tokens"] == s8spec and inc8[r]["tokens"] == inc8[0]["tokens"], r
     s8 = inc8[0]["tokens"]
@@ -115,7 +116,7 @@ def test_llama65b_80L_tp8_processes_vs_tp1(weight_init):
     lg8 = np.concatenate([inc8[r]["tf_logits"] for r in range(TP)], axis=1)  # vocab shards
     t8 = time.time() - t0
     # TP = 1 (the TP = 8 ranks have exited: their 130 GB are free again)
-    one = tp1_run(ps, max_length, tf_seqs, weight_init)
+    one = tp1_run(ps, max_length, tf_seqs, weight_init, spec_cfg)
     L = max_length
     assert lg8.shape == one["tf_logits"].shape == (len(tf_seqs) * L, 32000)
     nps = n_prompts + n_prompts
@@ -133,7 +134,7 @@ def test_llama65b_80L_tp8_processes_vs_tp1(weight_init):
                 spec_tp8_eq_tp1=sum(a == b for a, b in zip(s8spec, one["spec"])),
                 tp8_spec_eq_incr=sum(a == b for a, b in zip(s8spec, s8)),
                 tp1_spec_eq_incr=sum(a == b for a, b in zip(one["spec"], one["incr"])))
-    report(f"llama65b_80L_tp8_vs_tp1_{weight_init}", requests=len(ps), new_tokens=NEW,
+    report(f"llama65b_80L_tp8_vs_tp1_{weight_init}_{spec_cfg}", requests=len(ps), new_tokens=NEW,
            mismatches_vs_tp1=verdicts, exact=exact, total=total, tp8_seconds=round(t8, 1),
            incr_steps=one["incr_steps"], spec_steps=one["spec_steps"],
            tp8_spec_steps=spec8[0]["llm_steps"], sigma_pair_median=float(np.median(sig)),
