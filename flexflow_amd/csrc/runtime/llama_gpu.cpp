@@ -680,7 +680,18 @@ struct LlamaGPU : public ffmi_model {
   // largest one-item-per-request step that is graphed (FFMI_GRAPH_MAXT: A/B)
   int graph_max_t = getenv("FFMI_GRAPH_MAXT") ? atoi(getenv("FFMI_GRAPH_MAXT")) : 1024;
 
+  // forward = forward_launch (stage the step, enqueue it) + forward_finish
+  // (wait for it); SSM beam steps of several SSMs launch all, then finish
+  // each (serve_spec_infer), so their latency-bound steps overlap
+  bool inflight = false;
   ffmi_status forward(int k) {
+    ffmi_status st = forward_launch(k);
+    if (st != FFMI_OK) return st;
+    return forward_finish();
+  }
+
+  ffmi_status forward_launch(int k) {
+    inflight = false;
     const int T = (int)ps.tokens.size();
     prof_this_step = prof_level == 1 && (prof_steps++ % prof_every) == 0;
     ffmi_batch_desc desc;
@@ -730,6 +741,14 @@ struct LlamaGPU : public ffmi_model {
       st = enqueue(k, bytes, true);
       if (st != FFMI_OK) return st;
     }
+    inflight = true;
+    return FFMI_OK;
+  }
+
+  ffmi_status forward_finish() {
+    if (!inflight) return FFMI_OK;
+    inflight = false;
+    ffmi_status st;
     FFMI_HIP(hipStreamSynchronize(stream));
     // any attached transport (also under the RCCL path, whose chunks that fit
     // the exchange buffer still go over it) reports timeouts / errors here
@@ -971,13 +990,23 @@ struct LlamaGPU : public ffmi_model {
     return FFMI_OK;
   }
   ffmi_status run_beam(const BeamSearchBatchConfig &bc, BeamInferenceResult *ir) override {
+    ffmi_status st = beam_launch(bc);
+    if (st != FFMI_OK) return st;
+    return beam_collect(ir);
+  }
+  size_t beam_results = 0;  // results of the launched beam step (tokens x k)
+  ffmi_status beam_launch(const BeamSearchBatchConfig &bc) override {
     if (mode != FFMI_MODEL_BEAM) return FFMI_ERR_INVALID;
     FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
     pack_beam(bc, o.max_requests, slots, &ps);
     const int k = ps.topk;
-    ffmi_status st = forward(k);
+    beam_results = (size_t)bc.num_tokens * k;
+    return forward_launch(k);
+  }
+  ffmi_status beam_collect(BeamInferenceResult *ir) override {
+    ffmi_status st = forward_finish();
     if (st != FFMI_OK) return st;
-    const size_t n = (size_t)bc.num_tokens * k;
+    const size_t n = beam_results;
     memcpy(ir->token_ids, ids_h, n * sizeof(int32_t));
     memcpy(ir->probs, probs_h, n * sizeof(float));
     for (size_t i = 0; i < n; ++i) ir->parent_id[i] = 0;

@@ -48,6 +48,22 @@ struct ffmi_model {
                                ffmi::InferenceResult *ir) = 0;
   virtual ffmi_status run_beam(const ffmi::BeamSearchBatchConfig &bc,
                                ffmi::BeamInferenceResult *ir) = 0;
+  // A beam step in two halves, so that several SSMs' steps run at once
+  // (serve_spec_infer launches every SSM's step, then collects each):
+  // beam_launch enqueues the step of `bc` (which stays alive until the
+  // collect), beam_collect waits for it and writes the results.  Default:
+  // the synchronous run_beam at collect time.
+  virtual ffmi_status beam_launch(const ffmi::BeamSearchBatchConfig &bc) {
+    pending_beam = &bc;
+    return FFMI_OK;
+  }
+  virtual ffmi_status beam_collect(ffmi::BeamInferenceResult *ir) {
+    if (!pending_beam) return FFMI_ERR_INVALID;
+    const ffmi::BeamSearchBatchConfig *bc = pending_beam;
+    pending_beam = nullptr;
+    return run_beam(*bc, ir);
+  }
+  const ffmi::BeamSearchBatchConfig *pending_beam = nullptr;
   virtual ffmi_status set_profiling(int level) {
     (void)level;
     return FFMI_ERR_UNSUPPORTED;

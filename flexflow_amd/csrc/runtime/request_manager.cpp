@@ -1061,15 +1061,24 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
       break;
     }
     if (all_done()) break;
-    for (size_t s = 0; s < ssm_models.size() && st == FFMI_OK; s++) {
-      for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {
-        const double ts = now_us();
-        st = ssm_models[s]->run_beam((*beam_vec)[s], beam_ir);
-        stats.ssm_us += now_us() - ts;
-        if (st != FFMI_OK) break;
+    // MAX_BEAM_DEPTH beam steps per SSM (:3147-3159).  The reference runs
+    // SSM 0's steps, then SSM 1's ...; the SSMs are independent, so here
+    // every SSM's step d is launched before any is collected and their
+    // latency-bound steps overlap on their streams (identical batches and
+    // results: each SSM's chain of steps is unchanged)
+    for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && st == FFMI_OK; depth++) {
+      const double ts = now_us();
+      size_t launched = 0;
+      for (; launched < ssm_models.size() && st == FFMI_OK; launched++)
+        st = ssm_models[launched]->beam_launch((*beam_vec)[launched]);
+      for (size_t s = 0; s < launched; s++) {
+        const ffmi_status cs = ssm_models[s]->beam_collect(beam_ir);
+        if (st == FFMI_OK) st = cs;
+        if (st != FFMI_OK) continue;  // collect the rest: no step left in flight
         stats.ssm_steps++;
         (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
       }
+      stats.ssm_us += now_us() - ts;
     }
     if (st != FFMI_OK) break;
     *tree_bc = prepare_next_batch_verify(*beam_vec);
