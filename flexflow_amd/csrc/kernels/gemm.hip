@@ -749,7 +749,9 @@ __device__ __forceinline__ long long rt_now() { return __builtin_amdgcn_s_memrea
 
 template <int MTW, int NTW, int PF, int EPI, bool STAMP = false, bool XP = false, bool ULD = false,
           bool NTL = false>
-__global__ __launch_bounds__(256, NTW <= 8 ? 2 : 1) void gemm_mid_kernel(
+// (two workgroups per CU = 256 registers per wave: up to 24 accumulator tiles,
+// MTW x NTW; 4 x 8 takes the whole register file, one workgroup per CU)
+__global__ __launch_bounds__(256, NTW <= 8 && MTW * NTW <= 24 ? 2 : 1) void gemm_mid_kernel(
     const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp,
     uint16_t *__restrict__ Y, float *__restrict__ Ypart, int T, int N, int K, int KT,
     int NTILES, int S, int yp, size_t wts, size_t wks) {
@@ -944,10 +946,16 @@ __global__ void gemm_reduce_kernel(const float *__restrict__ Ypart, uint16_t *__
 struct MidPlan {
   int MTW, NTW, S, mblocks, nblk;
 };
+// FFMI_MID_MTW4=0: no 4-row-tile waves (A/B)
+static const int mid_mtw4 = getenv("FFMI_MID_MTW4") && atoi(getenv("FFMI_MID_MTW4")) == 0 ? 3 : 4;
 static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   MidPlan p;
   const int mtiles = (T + 15) / 16;
-  p.MTW = mtiles <= 8 ? 2 : 3;
+  // row tiles per wave: 4 waves x MTW tiles cover one row block; 4 for 13-16
+  // tiles (T 193-256: the width-4 verify step, T = 216, in ONE row block
+  // instead of two that each re-read every weight tile) and for prefill
+  // blocks (fewer row blocks re-reading the weights)
+  p.MTW = mtiles <= 8 ? 2 : mtiles <= 12 ? 3 : mtiles <= 16 || mtiles > 24 ? mid_mtw4 : 3;
   p.mblocks = (mtiles + 4 * p.MTW - 1) / (4 * p.MTW);
   const int KT = K / 32;
   const int ntiles = (N + 15) / 16 * (epi ? 2 : 1);
@@ -961,6 +969,7 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   static const int nopt = getenv("FFMI_MID_NARROW") && atoi(getenv("FFMI_MID_NARROW")) == 0 ? 4 : 6;
   for (int o = 6 - nopt; o < 6; ++o) {
     const int ntw = ntw_opts[o];
+    if (p.MTW == 4 && ntw > 8) continue;  // (register budget, see launch_gemm)
     const int nblk = (ntiles + ntw - 1) / ntw;
     for (int S = 1; S <= 8 && S <= KT; ++S) {
       const long wgs = (long)nblk * S * p.mblocks;
@@ -987,6 +996,14 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
   if (prefill_plan && p.mblocks >= 4) {
     p.NTW = 8;
     p.S = K >= 8192 && KT >= 2 ? 2 : 1;
+    // 4-row-tile waves run one workgroup per CU: only where the grid still
+    // covers the CUs (T = 1024: o_proj 128 workgroups -> 3-tile waves, 56 vs
+    // 70 us; gate/up, down (2 slices), qkv, lm_head keep 4: 267 vs 280 us,
+    // 131 vs 142 us, equal)
+    if (p.MTW == 4 && (long)((ntiles + 7) / 8) * p.S * p.mblocks < 256) {
+      p.MTW = 3;
+      p.mblocks = (mtiles + 11) / 12;
+    }
   }
   // diagnostics: FFMI_GEMM_PLAN="NTW,S" forces the tile width and split of
   // every M-split launch; "N:K:NTW,S;..." only of the listed shapes
@@ -1007,6 +1024,7 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       if (q) ++q;
     }
   }
+  if (p.MTW == 4 && p.NTW > 8) p.NTW = 8;
   p.nblk = (ntiles + p.NTW - 1) / p.NTW;
   return p;
 }
@@ -1150,6 +1168,12 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
 #define FFMI_RUN(M, NW) \
   return run_mid<M, NW, 4>(X, Wp, Y, ws, ws_bytes, T, N, K, epilogue, s, xp, yp, p.S, defer, nt, \
                            wpitch)
+    if (p.MTW == 4) {
+      if (p.NTW == 2) FFMI_RUN(4, 2);
+      if (p.NTW == 4) FFMI_RUN(4, 4);
+      if (p.NTW == 6) FFMI_RUN(4, 6);
+      FFMI_RUN(4, 8);  // (12 / 16 tiles: 4 x 16 accumulators exceed the register budget)
+    }
     if (p.MTW == 3) {
       if (p.NTW == 2) FFMI_RUN(3, 2);
       if (p.NTW == 4) FFMI_RUN(3, 4);

@@ -21,4 +21,7 @@ tests)
 bench)
   $S ext_bench 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 1
   ;;
+gemm)
+  $S ext_gemm 600 $PT --timeout 580 tests/test_gpu_llama_shapes.py tests/test_gpu_kernels.py -k "gemm or linear or shapes" || exit 1
+  ;;
 esac
