@@ -21,6 +21,12 @@ tests)
 bench)
   $S ext_bench 600 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline || exit 1
   ;;
+neg)
+  $S ext_neg 600 $PT --timeout 580 tests/test_gpu_bench_workload.py -k "negative" || exit 1
+  ;;
+65all)
+  $S ext_65all 1000 $PT --timeout 980 tests/test_gpu_llama65b_tp.py || exit 1
+  ;;
 gemm)
   $S ext_gemm 600 $PT --timeout 580 tests/test_gpu_llama_shapes.py tests/test_gpu_kernels.py -k "gemm or linear or shapes" || exit 1
   ;;
