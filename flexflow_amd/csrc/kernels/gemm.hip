@@ -880,6 +880,92 @@ __global__ __launch_bounds__(256, NTW <= 8 && MTW * NTW <= 24 ? 2 : 1) void gemm
   }
 }
 
+// Compute-bound form for prefill blocks (T >= 497, packed activations): one
+// 512-thread workgroup per 256 x 256 output tile, the 8 waves as 2 (rows) x
+// 4 (weight tiles), each wave 128 rows x 4 weight tiles (8 x 4 MFMA
+// accumulators).  Both operands are already in MFMA fragment order (1 KiB per
+// 16 x 32 fragment, weights.hip / pack_act_kernel), so every fragment lands in
+// LDS with ONE global_load_lds_dwordx4 wave-instruction (lane-linear: no
+// swizzle, conflict-free ds_read_b128 reads).  A ring of NB one-k-step stages
+// (32 fragments = 32 KiB each, 4 per wave) with NB - 1 stages in flight across
+// the barriers: a counted s_waitcnt vmcnt (never 0 in the steady state) and a
+// raw s_barrier, never __syncthreads (its fence would drain the DMAs; cdna
+// guide, "Pipelining across barriers").  The k order of every accumulator is
+// the M-split kernel's (k-steps in sequence, one MFMA each), so outputs are
+// bit-identical to gemm_mid_kernel at S = 1.  Blocks are remapped so the row
+// blocks of a weight tile share an XCD (bijective remap): its weights come
+// from HBM once per XCD L2.
+template <int EPI, int NB>
+__global__ __launch_bounds__(512, 1) void gemm_tile_kernel(
+    const uint16_t *__restrict__ X, const uint16_t *__restrict__ Wp, uint16_t *__restrict__ Y,
+    int T, int N, int KT, int NTILES, int MT, int nbm, int yp, size_t wts, size_t wks) {
+  __shared__ __attribute__((aligned(1024))) h8 lds[NB][32][64];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nwg = gridDim.x, b = blockIdx.x;
+  const int xcd = b & 7, q = nwg >> 3, r = nwg & 7;
+  const int L = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+  const int bn = L / nbm, bm = L % nbm;
+  // this wave's 4 DMA fragments f = wave + 8p of a stage: X m-tile f (< 16)
+  // or weight tile f - 16
+  const uint16_t *src[4];
+  size_t step[4];
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const int f = wave + 8 * p;
+    if (f < 16) {
+      src[p] = X + (size_t)min(bm * 16 + f, MT - 1) * KT * 512 + lane * 8;
+      step[p] = 512;
+    } else {
+      src[p] = Wp + (size_t)min(bn * 16 + f - 16, NTILES - 1) * wts + lane * 8;
+      step[p] = wks;
+    }
+  }
+  auto issue = [&](int kt) {
+    const int buf = kt % NB;
+#pragma unroll
+    for (int p = 0; p < 4; ++p)
+      __builtin_amdgcn_global_load_lds(
+          (const __attribute__((address_space(1))) void *)(src[p] + (size_t)kt * step[p]),
+          (__attribute__((address_space(3))) void *)(&lds[buf][wave + 8 * p][0]), 16, 0, 0);
+  };
+  const int wm = wave >> 2, wn = wave & 3;
+  f4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int kt = 0; kt < NB - 1; ++kt)
+    if (kt < KT) issue(kt);
+  for (int kt = 0; kt < KT; ++kt) {
+    // this wave's DMAs of step kt are done once at most the younger steps'
+    // (up to NB - 2 of them, 4 ops each) remain; then the barrier makes every
+    // wave's DMAs of step kt visible and retires every wave's reads of the
+    // buffer step kt + NB - 1 overwrites (step kt - 1's)
+    const int ahead = min(KT - 1 - kt, NB - 2);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kt + NB - 1 < KT) issue(kt + NB - 1);
+    const int buf = kt % NB;
+    h8 xf[8], wf[4];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) xf[i] = lds[buf][wm * 8 + i][lane];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wf[j] = lds[buf][16 + wn * 4 + j][lane];
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)  // D = W . X^T (see mid_store)
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wf[j], xf[i], acc[i][j], 0, 0, 0);
+  }
+  mid_store<8, 4, EPI>(acc, Y, nullptr, T, N, NTILES, 1, 0, bn * 16 + wn * 4,
+                       (bm * 16 + wm * 8) * 16, lane, yp);
+}
+
 static long long *stamp_buf() {
   static long long *buf = nullptr;
   if (!buf) {
@@ -1162,6 +1248,31 @@ hipError_t launch_gemm(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float
     if (fuse->kind == 1) FFMI_FZ(2, 1);
     FFMI_FZ(2, 2);
 #undef FFMI_FZ
+  }
+  // prefill blocks: the compute-bound 256 x 256 tile form where its grid
+  // covers the CUs (FFMI_TILE_GEMM: 0 never, 2 whenever the shape allows --
+  // A/B runs and tests; read per call)
+  if (mtiles >= 32 && xp && (!fuse || !fuse->kind)) {
+    const char *e = getenv("FFMI_TILE_GEMM");
+    const int mode = e ? atoi(e) : 1;
+    const int ntiles = (N + 15) / 16 * (epilogue ? 2 : 1);
+    const int nbn = (ntiles + 15) / 16, nbm = (mtiles + 15) / 16;
+    // one 256 x 256 tile per CU and round: worth it where the rounds are
+    // well filled (T = 1024: qkv 192 tiles 168 -> 140 us, lm_head 500 tiles
+    // 396 -> 314, gate/up 344 tiles 274 -> 268; T = 577: gate/up's 258 tiles
+    // = one round + 2, 188 -> 221, stays M-split)
+    const int nwg = nbn * nbm, rounds = (nwg + 255) / 256;
+    if (mode == 2 || (mode == 1 && nwg >= 160 && nwg * 10 >= rounds * 256 * 6)) {
+      if (defer) defer->S = 0;
+      const size_t wts = w_tile_stride(KT), wks = w_k_stride(wpitch ? wpitch : ntiles);
+      if (epilogue)
+        hipLaunchKernelGGL((gemm_tile_kernel<1, 4>), dim3(nbn * nbm), dim3(512), 0, s, X, Wp, Y, T,
+                           N, KT, ntiles, mtiles, nbm, yp, wts, wks);
+      else
+        hipLaunchKernelGGL((gemm_tile_kernel<0, 4>), dim3(nbn * nbm), dim3(512), 0, s, X, Wp, Y, T,
+                           N, KT, ntiles, mtiles, nbm, yp, wts, wks);
+      return hipGetLastError();
+    }
   }
   if (mtiles > 4) {
     const MidPlan p = mid_plan(T, N, K, epilogue, defer != nullptr && !epilogue);

@@ -27,6 +27,10 @@ neg)
 65all)
   $S ext_65all 1000 $PT --timeout 980 tests/test_gpu_llama65b_tp.py || exit 1
   ;;
+tile)
+  $S ext_tile 600 $PT --timeout 580 tests/test_gpu_llama_shapes.py -k "tile or 577 or 1024" || exit 1
+  bash scripts/gpu_kernel_ab.sh "scripts/gemm_bench.py --shapes llama7b --T 577,1024 --xpacked --wstream --iters 20" "" "FFMI_TILE_GEMM=0" "" || exit 1
+  ;;
 gemm)
   $S ext_gemm 600 $PT --timeout 580 tests/test_gpu_llama_shapes.py tests/test_gpu_kernels.py -k "gemm or linear or shapes" || exit 1
   ;;

@@ -93,3 +93,42 @@ def test_linear_at_baseline_shapes(shape, T):
     else:
         ref = O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1)
         close16(y, ref)
+
+
+@pytest.mark.parametrize("shape,T", [("7b_qkv", 1024), ("7b_o", 1024), ("7b_gate_up", 577),
+                                     ("7b_gate_up", 1024), ("7b_lm_head", 577),
+                                     ("7b_lm_head", 1024)])
+def test_tile_gemm_bit_identical_to_msplit(shape, T, monkeypatch):
+    """The compute-bound prefill form (gemm_tile_kernel: 256 x 256 tiles, LDS
+    fed by global_load_lds) against the M-split kernel on the same inputs:
+    both accumulate every output over the k-steps in sequence with the same
+    MFMA, so the outputs are bit-identical where the M-split side runs
+    unsplit (these shapes; where its planner splits K -- qkv / o at T = 577,
+    K = 8192 -- the orders differ and test_linear_at_baseline_shapes holds
+    both to the oracle)."""
+    N, K, epi = SHAPES[shape]
+    L = F.lib()
+    rng = np.random.default_rng(zlib.crc32(f"tile:{shape}:{T}".encode()))
+    X = f16(rng.standard_normal((T, K)))
+    rows = 2 * N if epi else N
+    W = f16(rng.uniform(-0.03, 0.03, (rows, K)))
+    Wp = Buf.empty((L.ffmi_linear_packed_bytes(rows, K) // 2,), np.uint16)
+    if epi:
+        gb, ub = Buf(np.ascontiguousarray(W[:N])), Buf(np.ascontiguousarray(W[N:]))
+        F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+    else:
+        src = Buf(W)
+        F.check(L.ffmi_linear_pack_weight(src.ptr, N, K, Wp.ptr, None))
+    Xp = Buf(pack_act_np(X))
+    Tp = (T + 15) // 16 * 16
+    out = {}
+    for mode in ("0", "2"):
+        monkeypatch.setenv("FFMI_TILE_GEMM", mode)
+        for yp in (0, 1):
+            flags = epi | F.X_PACKED | (F.Y_PACKED if yp else 0)
+            Y = Buf.empty(((Tp if yp else T), N), np.float16)
+            F.check(L.ffmi_linear(Xp.ptr, Wp.ptr, Y.ptr, T, N, K, flags, None), shape)
+            out[mode, yp] = Y.get()
+    for yp in (0, 1):
+        a, b = out["0", yp].view(np.uint16), out["2", yp].view(np.uint16)
+        assert np.array_equal(a, b), (yp, float((a != b).mean()))
