@@ -1068,6 +1068,7 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
     // results: each SSM's chain of steps is unchanged)
     for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && st == FFMI_OK; depth++) {
       const double ts = now_us();
+      double prep_us = 0;
       size_t launched = 0;
       for (; launched < ssm_models.size() && st == FFMI_OK; launched++)
         st = ssm_models[launched]->beam_launch((*beam_vec)[launched]);
@@ -1076,9 +1077,11 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
         if (st == FFMI_OK) st = cs;
         if (st != FFMI_OK) continue;  // collect the rest: no step left in flight
         stats.ssm_steps++;
+        const double tp = now_us();  // (host scheduling: not SSM step time)
         (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+        prep_us += now_us() - tp;
       }
-      stats.ssm_us += now_us() - ts;
+      stats.ssm_us += now_us() - ts - prep_us;
     }
     if (st != FFMI_OK) break;
     *tree_bc = prepare_next_batch_verify(*beam_vec);
