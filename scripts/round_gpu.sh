@@ -17,7 +17,7 @@ cd "$R"
 mkdir -p gpurun_out
 TAG=${TAG:-r02}
 P=/tmp/ffmi_prof_$TAG
-B="$R/bench.py --steps 1 --no-cpu-baseline --no-incr --profile 0"
+B="$R/bench.py --steps 1 --no-cpu-baseline --no-incr --no-legs --profile 0"
 run() { local n=$1 t=$2; shift 2; timeout -k 10 "$t" "$@" > "gpurun_out/$n.log" 2>&1; local rc=$?; echo "[$n] rc=$rc"; [ $rc -eq 0 ] || tail -n 20 "gpurun_out/$n.log"; return $rc; }
 run bench 400 python bench.py && grep '^{' gpurun_out/bench.log | tail -1 > "gpurun_out/${TAG}_bench.json" && \
 (export TMPDIR=/tmp DEBUG_CLR_GRAPH_PACKET_CAPTURE=0; cd /tmp && \
@@ -30,6 +30,6 @@ run bench 400 python bench.py && grep '^{' gpurun_out/bench.log | tail -1 > "gpu
  python3 "$R/scripts/pmc_table.py" "$P/pmcw/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_write_table.json" && echo "[pmc write] ok" && \
  timeout -k 10 400 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE --output-format csv -d "$P/mfma" -o bench -- python3 $B --warmup 0 > "$R/gpurun_out/pmc_mfma.log" 2>&1 && \
  python3 "$R/scripts/mfma_summary.py" "$P/mfma/bench_counter_collection.csv" > "$R/gpurun_out/${TAG}_pmc_mfma.json" && echo "[pmc_mfma] ok" && \
- timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/incr" -o incr -- python3 "$R/bench.py" --mode incr --steps 1 --warmup 1 --no-cpu-baseline --profile 0 > "$R/gpurun_out/incr_prof.log" 2>&1 && \
+ timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$P/incr" -o incr -- python3 "$R/bench.py" --mode incr --steps 1 --warmup 1 --no-cpu-baseline --no-legs --profile 0 > "$R/gpurun_out/incr_prof.log" 2>&1 && \
  cp "$P/incr/incr_kernel_stats.csv" "$R/gpurun_out/${TAG}_incr_kernel_stats.csv" && echo "[incr prof] ok") && \
-TAG=$TAG bash scripts/gpu_refresh_aux.sh
+{ [ "${SKIP_AUX:-0}" = 1 ] || TAG=$TAG bash scripts/gpu_refresh_aux.sh; }
