@@ -373,7 +373,14 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_init(
           new_bc.beamTokenInfo[new_bc.num_tokens].sub_request_index = 0;
           new_bc.num_tokens++;
           request.tokens.push_back(tk.first);
-          if (new_bc.num_tokens == max_tokens_per_batch) break;
+          // (the reference breaks here once the batch holds
+          // max_tokens_per_batch tokens, :1402-1404: the rest of this
+          // request's verified tokens never reach request.tokens although
+          // the LLM committed them, and later requests' tokens go past the
+          // limit anyway.  Every verified token is kept: an init batch holds
+          // at most max_requests x (MAX_BEAM_DEPTH + 1) tokens, which the SSM
+          // models are sized for, and a model smaller than that reports
+          // FFMI_ERR_INVALID instead of dropping tokens.)
         }
       }
     } else if (request.status == Request::PENDING) {
@@ -544,6 +551,13 @@ BeamSearchBatchConfig RequestManager::prepare_next_batch_beam(
       new_bc.causalMask[i].this_layer_size = 0;
       B.sub_request_num = 0;
       B.beam_size = 1;
+    } else if (max_tokens_per_batch - new_bc.num_tokens - max_requests_per_batch + i <= 0) {
+      // the running requests' beams took the batch: no prompt chunk in this
+      // beam step (the reference asserts in appendPendingRequest, :2431);
+      // a prompt that falls behind the LLM this way is reported as
+      // ssm_prompt_behind at the next init, as any other
+      R.num_tokens_in_batch = 0;
+      new_bc.causalMask[i].this_layer_size = 0;
     } else {
       R.num_tokens_in_batch =
           std::min(max_tokens_per_batch - new_bc.num_tokens - max_requests_per_batch + i,
@@ -587,12 +601,22 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
     else
       max_prompt_load_size -= 1;
   }
+  // later[i]: active requests after slot i.  Each keeps one token slot
+  // (a root or a prompt token), so a request's tree or prompt chunk never
+  // takes the last slots a later request needs.  The reference budgets
+  // MAX_BEAM_DEPTH + 1 tokens per running request (:1938-1946) although its
+  // trees hold up to ~21 and merged trees up to 64, and asserts when the batch
+  // overflows (:2137-2147); this only changes batches it would abort on.
+  std::vector<int> later(max_requests_per_batch, 0);
+  for (int i = max_requests_per_batch - 2; i >= 0; i--)
+    later[i] = later[i + 1] + (b0.request_completed[i + 1] ? 0 : 1);
   int num_active_req = -1;
   for (int i = 0; i < max_requests_per_batch; i++) {
     if (b0.request_completed[i]) continue;
     num_active_req++;
     const RequestGuid guid = b0.requestsInfo[i].request_guid;
     Request &request = all_requests[guid];
+    const int limit = max_verify - later[i];
     profiling_requests[guid].llm_decoding_steps += 1;
     auto &R = new_bc.requestsInfo[i];
     if (request.status == Request::RUNNING) {
@@ -630,7 +654,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
           (int)request.tokens.size() - 1;
       new_bc.num_tokens++;
       R.num_tokens_in_batch++;
-      assert(new_bc.num_tokens <= max_verify);
+      assert(new_bc.num_tokens <= limit);
       R.first_token_depth_in_request = (int)request.tokens.size() - 1;
       bool cutLayer = false;
       for (size_t j = 1; j < tree.size(); j++) {
@@ -639,7 +663,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
         new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = tree[j].second;
         new_bc.num_tokens++;
         R.num_tokens_in_batch++;
-        if (new_bc.num_tokens == max_verify && j != tree.size() - 1) {
+        if (new_bc.num_tokens == limit && j != tree.size() - 1) {
           cutLayer = true;
           break;
         }
@@ -679,8 +703,9 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
       R.max_length = b0.requestsInfo[i].max_length;
       new_bc.requestsInfo[num_active_req].batch_config_request_id = i;
       new_bc.request_completed[i] = false;
-      R.num_tokens_in_batch = std::min(max_prompt_load_size,
-                                       request.initial_len - R.first_token_depth_in_request);
+      R.num_tokens_in_batch = std::max(
+          0, std::min({max_prompt_load_size, limit - new_bc.num_tokens,
+                       request.initial_len - R.first_token_depth_in_request}));
       max_prompt_load_size -= R.num_tokens_in_batch;
       if (request.llm_cache_size < request.initial_len) {
         for (int j = 0; j < R.num_tokens_in_batch; j++) {
@@ -689,7 +714,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
           new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = request.llm_cache_size + j;
           new_bc.num_tokens++;
         }
-        assert(new_bc.num_tokens <= max_verify);
+        assert(new_bc.num_tokens <= limit);
         if (R.num_tokens_in_batch + request.llm_cache_size >= request.initial_len) {
           request.status = Request::RUNNING;
           new_bc.request_running[i] = true;
@@ -698,7 +723,7 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
               TokenDepth(request.tokens.back(), (int)request.tokens.size() - 1)};
           dfs_tree_parents[guid] = std::vector<int>{-1};
         }
-      } else if (max_verify - new_bc.num_tokens > 0) {
+      } else if (limit - new_bc.num_tokens > 0) {
         // whole prompt cached: launch the request with its last token
         request.status = Request::RUNNING;
         new_bc.request_running[i] = true;
@@ -936,10 +961,20 @@ std::vector<RequestManager::TokenDepth> RequestManager::merge_dfs_trees(
     const std::vector<std::vector<TokenDepth>> &trees, int root_depth, RequestGuid guid) {
   (void)root_depth;
   assert(!trees.empty());
+  const int cap = std::max(1, std::min(max_spec_tree_token_num,
+                                       (int)BatchConfig::MAX_SPEC_TREE_TOKEN_NUM));
   if (trees.size() == 1) {
-    dfs_tree_inputs[guid] = trees[0];
-    dfs_tree_parents[guid] = layer_order_parents(trees[0]);
-    return trees[0];
+    // (cut to the cap like a merged tree: a tree larger than the models' KV
+    // tail -- max_seq_len + max_spec_tree_token_num slots per request -- has
+    // nowhere to store its last nodes; e.g. widths (4,) grow 1 + 4 x 8 = 33
+    // nodes.  The reference places such a tree whole.  A layer-order prefix
+    // keeps every node's ancestors.)
+    std::vector<TokenDepth> t = trees[0];
+    std::vector<int> par = layer_order_parents(t);
+    if ((int)t.size() > cap) t.resize(cap), par.resize(cap);
+    dfs_tree_inputs[guid] = t;
+    dfs_tree_parents[guid] = par;
+    return t;
   }
   struct Node {
     TokenDepth td;
@@ -965,8 +1000,6 @@ std::vector<RequestManager::TokenDepth> RequestManager::merge_dfs_trees(
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) {
     return nodes[a].td.second < nodes[b].td.second;
   });
-  const int cap = std::max(1, std::min(max_spec_tree_token_num,
-                                       (int)BatchConfig::MAX_SPEC_TREE_TOKEN_NUM));
   if ((int)order.size() > cap) order.resize(cap);
   std::vector<int> pos(nodes.size(), -1);
   for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;

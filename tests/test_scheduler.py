@@ -57,11 +57,12 @@ def run_incr(ps, max_length, batch=4, max_tokens=16, eos=()):
 
 
 def run_spec(ps, max_length, batch=4, max_tokens=64, widths=(1, 1, 3), disagree=0,
-             tree_tokens=23, ssms=None, ext=0):
+             tree_tokens=23, ssms=None, ext=0, eos=()):
     """ssms: [(salt, disagree_pct)] per SSM (default one SSM, salt 1234)."""
     rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
                            max_sequence_length=128, spec_tree_width=widths,
-                           max_spec_tree_token_num=tree_tokens, spec_extensions=ext)
+                           max_spec_tree_token_num=tree_tokens, spec_extensions=ext,
+                           eos_token_ids=eos)
     llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=128,
                        max_tree_tokens=tree_tokens)
     for salt, dis in ssms or [(1234, disagree)]:
@@ -248,3 +249,87 @@ def test_multi_ssm_merge_keeps_the_agreeing_branch():
 def test_multi_ssm_needs_the_extension_flag():
     with pytest.raises(fa.ffmi.FFMIError, match="UNSUPPORTED|unsupported"):
         run_spec(prompts(2, V), 40, ssms=[(1, 0), (2, 0)])
+
+
+@pytest.mark.parametrize("tree_tokens", [23, 48])
+def test_multi_ssm_chunked_prompts_and_queueing(tree_tokens):
+    """The extensions under the scheduler's other paths: more requests than
+    batch slots and prompts longer than the token budget, loaded in chunks by
+    the LLM and by every SSM.  Round 5 found two batch-capacity bugs here, both
+    the reference's own accounting: a verify batch that overflowed (prompt
+    chunks budgeted at MAX_BEAM_DEPTH + 1 tokens per running request, trees
+    larger than that; the reference asserts, :2137-2147) and verified tokens
+    dropped from request.tokens once the next init batch held
+    max_tokens_per_batch tokens (:1402-1404)."""
+    ps = prompts(9, V, lo=30, hi=60, seed=5)
+    res, st = run_spec(ps, 100, batch=3, max_tokens=24, tree_tokens=tree_tokens,
+                       ssms=[(1234, 20), (99, 40), (7, 100)], ext=MULTI)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 100, V), tree_tokens
+    assert st.ssm_steps > 0
+
+
+def test_spec_infer_ignores_eos_like_the_reference():
+    """SpecInfer completes a request on max_length only: the verify path never
+    checks EOS (request_manager.cc:1251-1253), unlike incremental decoding
+    (:650-655, :771-774).  The same holds here, one SSM or several."""
+    ps = prompts(4, V, seed=3)
+    eos = expected(ps[0], 70, V)[len(ps[0]) + 5]
+    for ssms, ext in (([(1234, 20)], 0), ([(1234, 20), (99, 40)], MULTI)):
+        res, _ = run_spec(ps, 70, ssms=ssms, ext=ext, eos=(eos,))
+        for p, r in zip(ps, res):
+            assert r.output_tokens == expected(p, 70, V)  # EOS not applied
+    inc, _ = run_incr(ps, 70, eos=(eos,))
+    assert inc[0].output_tokens == expected(ps[0], 70, V, eos=(eos,))
+    assert len(inc[0].output_tokens) < 70
+
+
+WIDTHS = [(1, 1, 3), (3,), (1, 2), (2, 1, 1), (1, 1, 4), (4,), (2, 2), (1, 4), (2, 1, 2), ()]
+
+
+@pytest.mark.parametrize("block", range(10))
+def test_spec_infer_randomized_configs_equal_incr(block):
+    """Randomised scheduler configurations (batch slots, token budget, tree
+    widths up to 4, tree budget, 1-4 SSMs with different agreement, 1-10
+    requests, prompt lengths, max_length): SpecInfer reproduces incremental
+    decoding exactly.  Configurations whose prompts the SSM cannot load in
+    time raise the reported FFMI error (the reference asserts) and are
+    skipped."""
+    import random
+    checked = 0
+    for seed in range(block * 40, block * 40 + 40):
+        r = random.Random(seed)
+        batch = r.choice([1, 2, 3, 4, 8])
+        mt = r.choice([8, 16, 24, 32, 64, 128])
+        widths = r.choice(WIDTHS)
+        nssm = r.choice([1, 1, 2, 3, 4])
+        tree = r.choice([16, 23, 27, 32, 48, 64])
+        ssms = [(r.randrange(1, 10000), r.choice([0, 10, 30, 60, 100])) for _ in range(nssm)]
+        ps = prompts(r.randint(1, 10), V, lo=2, hi=max(3, min(2 * mt, 60)), seed=seed)
+        ml = min(127, max(r.choice([40, 70, 100, 127]), max(len(p) for p in ps) + 3))
+        try:
+            res, _ = run_spec(ps, ml, batch=batch, max_tokens=mt, widths=widths,
+                              tree_tokens=tree, ssms=ssms, ext=W4 | (MULTI if nssm > 1 else 0))
+        except fa.ffmi.FFMIError as e:
+            assert "SSM loaded less" in str(e), (seed, str(e))
+            continue
+        for p, q in zip(ps, res):
+            assert q.output_tokens == expected(p, ml, V), seed
+        checked += 1
+    assert checked >= 25
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_incr_decoding_randomized_configs(seed):
+    """Incremental decoding under random slots / token budgets / EOS: equal
+    to greedy decoding with the EOS dropped (request_manager.cc:771-774)."""
+    import random
+    r = random.Random(1000 + seed)
+    ps = prompts(r.randint(1, 12), V, lo=1, hi=50, seed=seed)
+    ml = r.choice([60, 90, 127])
+    full = expected(ps[0], ml, V)
+    eos = (full[len(ps[0]) + r.randint(1, 8)],) if r.random() < 0.7 else ()
+    res, _ = run_incr(ps, ml, batch=r.choice([1, 2, 3, 5, 8]), max_tokens=r.choice([4, 7, 16, 64]),
+                      eos=eos)
+    for p, q in zip(ps, res):
+        assert q.output_tokens == expected(p, ml, V, eos=eos), seed
