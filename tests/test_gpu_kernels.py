@@ -660,6 +660,125 @@ def test_attention_tree_fused_equals_two_launch_path(d, monkeypatch):
         assert np.array_equal(np.asarray(b).view(np.uint16), np.asarray(c).view(np.uint16))
 
 
+def random_layer_tree(rng, n, max_width=4):
+    """A random token tree of n nodes in layer order (the scheduler's
+    serialisation): parents precede children, depths non-decreasing."""
+    parents, depth = [-1], [0]
+    layer = [0]
+    while len(parents) < n:
+        nxt = []
+        for p in layer:
+            for _ in range(int(rng.integers(1, max_width + 1))):
+                if len(parents) == n:
+                    break
+                parents.append(p)
+                depth.append(depth[p] + 1)
+                nxt.append(len(parents) - 1)
+        layer = nxt or [len(parents) - 1]
+    return parents, depth
+
+
+@pytest.mark.parametrize("path", ["default", "qsplit", "two_launch"])
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("seed", range(6))
+def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
+    """Tree verification at random shapes against the oracle: 1-4 requests
+    with random prompt lengths (crossing the 32-key chunks and the LDS tail),
+    random layer-order trees of 1-64 nodes (the merged multi-SSM bound: mask
+    bit 63; trees over 32 nodes take two work items and the two-launch path),
+    then a step that commits a random accepted path and verifies a fresh
+    random tree -- every query row checked against O.attention_row (the
+    exact-fraction bar over all rows of the test, not per 128-element row);
+    through the default launch, the query-split one (the TP >= 2 form) and
+    the KV-update + attention pair."""
+    if path == "qsplit":
+        monkeypatch.setenv("FFMI_ATTN_QSPLIT", "2")
+    elif path == "two_launch":
+        monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
+    rng = np.random.default_rng(1000 + 10 * d + seed)
+    R = int(rng.integers(1, 5))
+    c = AttnCase(F.ATTN_TREE, d=d, max_requests=4, max_seq=200, tree=64, max_tokens=512)
+    plen = {r: int(rng.integers(1, 100)) for r in range(R)}
+    infos = [(3, p, r, p, p + 1, 0, 0, 0) for r in range(R) for p in range(plen[r])]
+    out, qs = c.run(infos, masks=[[0]] * R, rng=rng)
+    got, want = [], []
+    for t, i in enumerate(infos):
+        got.append(out[t])
+        want.append(c.ref_row(qs[t], i[2], range(i[1] + 1)))
+    ntcs = dict(plen)
+    commits = []
+    for step in range(2):
+        trees, infos, masks = {}, [], []
+        for r in range(R):
+            n = int(rng.choice([1, 2, 7, 21, 27, 33, 48, 63, 64]))
+            parents, depth = random_layer_tree(rng, n)
+            trees[r] = (parents, depth, len(infos))
+            masks.append(tree_masks(parents))
+            infos += [(4, ntcs[r] + depth[j], r, ntcs[r] + j, ntcs[r], ntcs[r], n, j)
+                      for j in range(n)]
+        out, qs = c.run(infos, masks=masks, commits=commits, rng=rng)
+        for r in range(R):
+            parents, depth, off = trees[r]
+            for j in range(len(parents)):
+                anc, a = [], j
+                while a >= 0:
+                    anc.append(ntcs[r] + a)
+                    a = parents[a]
+                got.append(out[off + j])
+                want.append(c.ref_row(qs[off + j], r, list(range(ntcs[r])) + sorted(anc)))
+        # accept a random root-to-node path per request: commit it in order
+        commits = []
+        for r in range(R):
+            parents, depth, off = trees[r]
+            a, path = int(rng.integers(0, len(parents))), []
+            while a >= 0:
+                path.append(a)
+                a = parents[a]
+            for k, j in enumerate(reversed(path)):
+                commits.append((off + j, r, ntcs[r] + k))
+            ntcs[r] += len(path)
+    c.check(np.stack(got), np.stack(want))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_attention_spec_random_beam_trees_vs_oracle(seed):
+    """SSM beam steps at random shapes (the 68M SSM's d = 64): 1-4 requests
+    with random prompts, then one step per tree layer -- the layer's nodes are
+    the queries, earlier layers already stored by earlier steps -- over random
+    layer-order trees of up to 64 nodes (widths up to 4, merged-tree sizes);
+    every query row against O.attention_row over its prefix + ancestors
+    (the exact-fraction bar over all rows of the test)."""
+    rng = np.random.default_rng(2000 + seed)
+    R = int(rng.integers(1, 5))
+    c = AttnCase(F.ATTN_SPEC, d=64, max_requests=4, max_seq=160, tree=64, max_tokens=512)
+    plen = {r: int(rng.integers(1, 100)) for r in range(R)}
+    infos = [(3, p, r, p, p + 1, 0, 0, 0) for r in range(R) for p in range(plen[r])]
+    c.run(infos, masks=[[0]] * R, rng=rng)
+    got, want = [], []
+    trees = {r: random_layer_tree(rng, int(rng.choice([2, 9, 21, 33, 64]))) for r in range(R)}
+    masks = [tree_masks(trees[r][0]) for r in range(R)]
+    depth_max = max(max(trees[r][1]) for r in range(R))
+    for layer in range(depth_max + 1):  # the root (layer 0) first
+        infos, who = [], []
+        for r in range(R):
+            parents, depth = trees[r]
+            nodes = [j for j in range(len(parents)) if depth[j] == layer]
+            if not nodes:
+                continue
+            ntcs, tl = plen[r], nodes[-1] + 1  # stored so far: layers <= this one
+            infos += [(5, ntcs + layer, r, ntcs + j, ntcs, ntcs, tl, j) for j in nodes]
+            who += [(r, j) for j in nodes]
+        out, qs = c.run(infos, masks=masks, rng=rng)
+        for t, (r, j) in enumerate(who):
+            anc, a = [], j
+            while a >= 0:
+                anc.append(plen[r] + a)
+                a = trees[r][0][a]
+            got.append(out[t])
+            want.append(c.ref_row(qs[t], r, list(range(plen[r])) + sorted(anc)))
+    c.check(np.stack(got), np.stack(want))
+
+
 @pytest.mark.parametrize("fp32", [False, True])
 def test_attention_spec_beam_layers(fp32):
     rng = np.random.default_rng(7)
