@@ -192,6 +192,64 @@ def test_linear_gate_up_silu_fused(T):
     close16(Yb.get(), ref, max_ulp=3, exact_frac=0.99, atol=1e-3)
 
 
+@pytest.mark.parametrize("seed", range(20))
+def test_linear_random_shapes_vs_oracle(seed):
+    """ffmi_linear at random shapes against the oracle: T 1-1100 (skinny,
+    wave, M-split with 2-4 row tiles per wave and split K, the 256 x 256 tile
+    form), N from 16 to 20000 (ragged: not a multiple of 16 or 32), K a
+    multiple of 32 up to 8192, with and without the SiLU-mul epilogue, row-
+    major or packed activations in and out, weight-stream hint on or off."""
+    rng = np.random.default_rng(4242 + seed)
+    for _ in range(3):
+        T = int(np.exp(rng.uniform(0, np.log(1100))))
+        N = int(rng.choice([int(rng.integers(16, 400)), int(rng.integers(400, 6000)),
+                            int(rng.integers(6000, 20000))]))
+        K = 32 * int(np.exp(rng.uniform(0, np.log(256))))
+        epi = int(rng.integers(0, 2))
+        xp = int(rng.integers(0, 2))
+        yp = int(rng.integers(0, 2)) if N % 32 == 0 else 0
+        flags = (F.EPI_SILU_MUL if epi else F.EPI_NONE) | (F.W_STREAM if rng.integers(0, 2) else 0)
+        X = f16(rng.standard_normal((T, K)))
+        sc = 1.0 / np.sqrt(K)
+        if epi:
+            Wg = f16(rng.uniform(-2 * sc, 2 * sc, (N, K)))
+            Wu = f16(rng.uniform(-2 * sc, 2 * sc, (N, K)))
+            gb, ub = Buf(Wg), Buf(Wu)
+            Wp = Buf.empty((2 * L.ffmi_linear_packed_bytes(N, K) // 2,), np.uint16)
+            F.check(L.ffmi_linear_pack_gate_up(gb.ptr, ub.ptr, N, K, Wp.ptr, None))
+        else:
+            W = f16(rng.uniform(-2 * sc, 2 * sc, (N, K)))
+            Wp = packed(W)
+        Xb = Buf(pack_act_np(X)) if xp else Buf(X)
+        Tp = (T + 15) // 16 * 16
+        Yb = Buf.empty(((Tp if yp else T), N), np.float16)
+        flags |= (F.X_PACKED if xp else 0) | (F.Y_PACKED if yp else 0)
+        F.check(L.ffmi_linear(Xb.ptr, Wp.ptr, Yb.ptr, T, N, K, flags, None), (T, N, K, flags))
+        y = unpack_act_np(Yb.get().reshape(-1), T, N) if yp else Yb.get()
+        if epi:
+            g = O.linear(X.astype(np.float32), Wg.astype(np.float32))
+            u = O.linear(X.astype(np.float32), Wu.astype(np.float32))
+            # the gate/up box check of test_gpu_llama_shapes: >= 98% bit-
+            # identical to the chain on the oracle's fp16 gate/up, the rest
+            # inside the chain's range over gate/up within the plain GEMM
+            # tolerance (a one-ulp flip of g near silu's flat region moves y
+            # by several ulps) + 1 output ulp
+            g16, u16 = g.astype(np.float16), u.astype(np.float16)
+            chain = lambda a, b: O.silu_mul(a.astype(np.float32), b.astype(np.float32))  # noqa: E731
+            y16 = y.astype(np.float16)
+            assert (y16 == chain(g16, u16).astype(np.float16)).mean() >= 0.98
+            sp = lambda a: np.spacing(np.abs(a).astype(np.float16)).astype(np.float32)  # noqa: E731
+            dg = np.maximum(2 * sp(g16), 1e-4 * np.abs(g).max())
+            du = np.maximum(2 * sp(u16), 1e-4 * np.abs(u).max())
+            pts = [chain(g + a * dg, u + b * du) for a in (-1, 0, 1) for b in (-1, 0, 1)]
+            lo, hi = np.min(pts, axis=0), np.max(pts, axis=0)
+            slack = sp(np.maximum(np.abs(lo), np.abs(hi)))
+            yf = y16.astype(np.float32)
+            assert not ((yf < lo - slack) | (yf > hi + slack)).any(), (T, N, K, flags)
+        else:
+            close16(y, O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1))
+
+
 @pytest.mark.parametrize("Ts", [(1, 8, 40, 64), (65, 100, 168, 192)])
 @pytest.mark.parametrize("wstream", [0, 1])
 @pytest.mark.parametrize("K", [1024, 1536, 2048])
@@ -336,6 +394,53 @@ def test_softmax_argmax_topk_exact(V):
         rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
         assert np.array_equal(ids.get(), rid)
         np.testing.assert_array_equal(pr.get(), rp)
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_softmax_topk_random_shapes_exact(seed):
+    """Softmax + argmax / top-k (k 1-4) at random shapes, bit-exact against
+    the oracle: T 1-300, V from 64 to 140000 (multiples of 8 take the
+    register kernel, others and V > 32768 the streaming one), logit scales
+    from flat (fp16 p collapses, many candidates) to peaked, planted ties."""
+    rng = np.random.default_rng(777 + seed)
+    T = int(rng.integers(1, 301))
+    V = int(rng.choice([int(rng.integers(8, 4096)) * 8, int(rng.integers(64, 40000)),
+                        32000, 32001, int(rng.integers(32769, 140000))]))
+    scale = float(rng.choice([1e-3, 0.05, 1.0, 3.0, 8.0]))
+    logits = f16(rng.standard_normal((T, V)) * scale)
+    for t in rng.choice(T, size=min(T, 4), replace=False):  # planted exact ties
+        m = f16(float(np.abs(logits[t]).max()) + 1.0)
+        logits[t, rng.choice(V, size=int(rng.integers(2, 6)), replace=False)] = m
+    lb = Buf(logits)
+    k = int(rng.integers(1, 5))
+    ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+    F.check(L.ffmi_arg_topk(lb.ptr, T, V, k, ids.ptr, pr.ptr, None), (T, V, k))
+    rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+    assert np.array_equal(ids.get(), rid.reshape(T, k)), (T, V, k, scale)
+    np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_rmsnorm_random_shapes(seed):
+    """RMSNorm / residual RMSNorm at random T (1-1100) and H (multiple of 8
+    up to 16384): residual bit-exact, output within 1 fp16 ulp of the
+    oracle and >= 99% bit-identical."""
+    rng = np.random.default_rng(555 + seed)
+    T = int(np.exp(rng.uniform(0, np.log(1100))))
+    H = 8 * int(rng.integers(1, 2049))
+    x1 = f16(rng.standard_normal((T, H)) * float(rng.choice([0.01, 1.0, 30.0])))
+    x2 = f16(rng.standard_normal((T, H)))
+    w = f16(1 + rng.uniform(-0.5, 0.5, H))
+    eps = float(rng.choice([1e-6, 1e-5]))
+    b1, b2, bw = Buf(x1), Buf(x2), Buf(w)
+    out, res = Buf.empty((T, H), np.float16), Buf.empty((T, H), np.float16)
+    F.check(L.ffmi_rmsnorm(b1.ptr, bw.ptr, out.ptr, T, H, eps, None))
+    close16(out.get(), O.rmsnorm(x1.astype(np.float32), w.astype(np.float32), eps), 1, 0.99)
+    F.check(L.ffmi_residual_rmsnorm(b1.ptr, b2.ptr, bw.ptr, res.ptr, out.ptr, T, H, eps, None))
+    r_ref, o_ref = O.residual_rmsnorm(x1.astype(np.float32), x2.astype(np.float32),
+                                      w.astype(np.float32), eps)
+    assert np.array_equal(res.get().view(np.uint16), f16(r_ref).view(np.uint16))
+    close16(out.get(), o_ref, 1, 0.99)
 
 
 @pytest.mark.parametrize("T,V", [(24, 32000), (200, 32000), (3, 4096), (5, 65536)])
