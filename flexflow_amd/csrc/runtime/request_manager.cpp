@@ -1096,23 +1096,36 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
     if (all_done()) break;
     // MAX_BEAM_DEPTH beam steps per SSM (:3147-3159).  The reference runs
     // SSM 0's steps, then SSM 1's ...; the SSMs are independent, so here
-    // every SSM's step d is launched before any is collected and their
-    // latency-bound steps overlap on their streams (identical batches and
-    // results: each SSM's chain of steps is unchanged)
-    for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && st == FFMI_OK; depth++) {
+    // their latency-bound steps overlap on their streams: every SSM's step 0
+    // is launched, then each SSM's step d + 1 goes out as soon as its step d
+    // is collected and its next batch prepared, while the other SSMs' steps
+    // d are still running (identical batches and results: each SSM's chain
+    // of steps is unchanged)
+    {
+      const size_t n = ssm_models.size();
       const double ts = now_us();
       double prep_us = 0;
-      size_t launched = 0;
-      for (; launched < ssm_models.size() && st == FFMI_OK; launched++)
-        st = ssm_models[launched]->beam_launch((*beam_vec)[launched]);
-      for (size_t s = 0; s < launched; s++) {
-        const ffmi_status cs = ssm_models[s]->beam_collect(beam_ir);
-        if (st == FFMI_OK) st = cs;
-        if (st != FFMI_OK) continue;  // collect the rest: no step left in flight
-        stats.ssm_steps++;
-        const double tp = now_us();  // (host scheduling: not SSM step time)
-        (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
-        prep_us += now_us() - tp;
+      std::vector<bool> inflight(n, false);
+      for (size_t s = 0; s < n && st == FFMI_OK; s++) {
+        st = ssm_models[s]->beam_launch((*beam_vec)[s]);
+        inflight[s] = st == FFMI_OK;
+      }
+      for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {
+        for (size_t s = 0; s < n; s++) {
+          if (!inflight[s]) continue;
+          inflight[s] = false;
+          const ffmi_status cs = ssm_models[s]->beam_collect(beam_ir);
+          if (st == FFMI_OK) st = cs;
+          if (st != FFMI_OK) continue;  // collect the rest: no step left in flight
+          stats.ssm_steps++;
+          const double tp = now_us();  // (host scheduling: not SSM step time)
+          (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+          prep_us += now_us() - tp;
+          if (depth + 1 < BeamSearchBatchConfig::MAX_BEAM_DEPTH) {
+            st = ssm_models[s]->beam_launch((*beam_vec)[s]);
+            inflight[s] = st == FFMI_OK;
+          }
+        }
       }
       stats.ssm_us += now_us() - ts - prep_us;
     }
