@@ -1,0 +1,111 @@
+"""Randomised end-to-end GPU parity: small LLaMA models of random shape
+(1-3 layers, 1-8 heads of d = 64 or 128, random FFN width and vocabulary,
+RoPE theta, RMS eps), random scheduler limits (batch slots, token budget) and
+random request mixes (1-10 prompts of 1-60 tokens, queued past the slots),
+through the MI355X path:
+
+  * incremental decoding: every request's tokens teacher-forced through the
+    oracle, under test_gpu_e2e's tie rule (a mismatch must be a tie of the
+    two tokens' fp16 probabilities within 2 ulp), with the ties of a test
+    capped at max(2, 3%) of its picks (the tie cap of tests/parity_rules.py;
+    first run: 5 ties in 4281 tokens, at most 2 in one sequence);
+  * SpecInfer with 1-2 random SSMs (the multi-SSM merge under
+    FFMI_SPEC_EXT_MULTI_SSM) and random tree widths up to 4: its tokens under
+    the same rule -- so SpecInfer equals incremental decoding up to ties.
+"""
+import numpy as np
+import pytest
+
+import flexflow_amd as fa
+from test_gpu_e2e import check_tokens_vs_oracle
+
+
+def check_all(cfg, seed, ps, res, ml, what):
+    """every request under the tie rule; the test's ties capped at max(2, 3%)"""
+    ties = total = 0
+    for p, r in zip(ps, res):
+        assert len(r.output_tokens) == ml, what
+        n = len(r.output_tokens) - (len(p) + 1)
+        ties += n - check_tokens_vs_oracle(cfg, seed, r.output_tokens, len(p) + 1,
+                                           max_tie_frac=1.0)
+        total += n
+    assert ties <= max(2, 0.03 * total), (ties, total, what)
+
+pytestmark = pytest.mark.gpu
+
+WIDTHS = [(1, 1, 3), (3,), (2, 1, 1), (1, 1, 4), (2, 2), ()]
+
+
+def random_cfg(rng, vocab=None):
+    heads = int(rng.choice([1, 2, 4, 8]))
+    d = int(rng.choice([64, 128]))
+    return dict(num_layers=int(rng.integers(1, 4)),
+                vocab_size=int(vocab or rng.integers(100, 5000)),
+                num_heads=heads, num_kv_heads=heads, hidden=heads * d,
+                intermediate=32 * int(rng.integers(2, 48)),
+                rms_eps=float(rng.choice([1e-6, 1e-5])),
+                rope_theta=float(rng.choice([10000.0, 500000.0])))
+
+
+def random_requests(rng, V):
+    n = int(rng.integers(1, 11))
+    ps = [rng.integers(3, V, size=int(rng.integers(1, 61))).tolist() for _ in range(n)]
+    max_length = min(127, max(len(p) for p in ps) + 1 + int(rng.integers(8, 40)))
+    return ps, max_length
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_model_incr_decoding_vs_oracle(seed):
+    rng = np.random.default_rng(9000 + seed)
+    cfg = random_cfg(rng)
+    ps, ml = random_requests(rng, cfg["vocab_size"])
+    B = int(rng.choice([1, 2, 3, 4, 8]))
+    mtb = int(rng.choice([8, 16, 32, 64, 128]))
+    rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                           max_sequence_length=128)
+    m = fa.Model(cfg, "inc", max_requests=B, max_tokens=mtb, max_seq_len=128,
+                 weight_seed=100 + seed)
+    try:
+        res = fa.generate(rm, m, ps, max_length=ml)
+    finally:
+        m.close()
+    check_all(cfg, 100 + seed, ps, res, ml, (cfg, B, mtb))
+
+
+@pytest.mark.parametrize("seed", range(20))
+def test_random_model_spec_infer_vs_oracle(seed):
+    rng = np.random.default_rng(9500 + seed)
+    cfg = random_cfg(rng)
+    V = cfg["vocab_size"]
+    ps, ml = random_requests(rng, V)
+    B = int(rng.choice([1, 2, 4, 8]))
+    mtb = int(rng.choice([32, 64, 128]))
+    widths = WIDTHS[int(rng.integers(0, len(WIDTHS)))]
+    nssm = int(rng.integers(1, 3))
+    tree = 64 if nssm > 1 else 33
+    ext = fa.ffmi.SPEC_EXT_WIDTH4 | (fa.ffmi.SPEC_EXT_MULTI_SSM if nssm > 1 else 0)
+    vt = mtb + tree * B
+    rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                           max_sequence_length=128, spec_tree_width=widths,
+                           max_spec_tree_token_num=tree, spec_extensions=ext)
+    llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
+                   max_tree_tokens=tree, weight_seed=200 + seed)
+    # SSMs: random smaller models over the same vocabulary, or (agreeing
+    # fully) the LLM's own shape and weights, for long accepted paths
+    ssms = []
+    for k in range(nssm):
+        same = rng.random() < 0.3
+        scfg = cfg if same else random_cfg(rng, vocab=V)
+        ssms.append(fa.Model(scfg, "beam", max_requests=B, max_tokens=vt, max_seq_len=128,
+                             max_tree_tokens=tree, weight_seed=200 + seed if same else 300 + k))
+        rm.register_ssm_model(ssms[-1])
+    try:
+        res = fa.generate(rm, llm, ps, max_length=ml, spec=True)
+    except fa.ffmi.FFMIError as e:  # a prompt the SSM cannot load in time (the
+        assert "SSM loaded less" in str(e)  # reference asserts): not a parity case
+        pytest.skip("SSM prompt behind the LLM for this random mix")
+    finally:
+        llm.close()
+        for s in ssms:
+            s.close()
+    check_all(cfg, 200 + seed, ps, res, ml, (cfg, B, mtb, widths, nssm))
