@@ -89,6 +89,36 @@ def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
                                max_tie_frac=0.1)
 
 
+@pytest.mark.parametrize("seed", range(6))
+def test_peer_tp_random_models(seed):
+    """TP 2 or 4 over the transport at random small LLaMA shapes (heads a
+    multiple of TP, d 64 / 128, FFN and vocabulary random: the vocabulary
+    sharded when V/TP is a multiple of 16, else the unsharded tail), random
+    prompts, overlap on or off, incremental decoding or SpecInfer: every rank
+    emits the same tokens, oracle-valid picks of the UNSHARDED model under
+    the TP tie rule of test_peer_tp_model_decodes_like_unsharded."""
+    from test_gpu_e2e import SSM_CFG, check_tokens_vs_oracle
+    rng = np.random.default_rng(4100 + seed)
+    tp = int(rng.choice([2, 4]))
+    heads = tp * int(rng.integers(1, 3))
+    d = int(rng.choice([64, 128]))
+    V = int(rng.choice([16 * tp * int(rng.integers(8, 120)), int(rng.integers(200, 3000))]))
+    cfg = dict(num_layers=int(rng.integers(1, 3)), vocab_size=V, num_heads=heads,
+               num_kv_heads=heads, hidden=heads * d, intermediate=32 * tp * int(rng.integers(1, 12)),
+               rms_eps=1e-6, rope_theta=10000.0)
+    ps = [rng.integers(3, V, size=int(rng.integers(2, 40))).tolist()
+          for _ in range(int(rng.integers(1, 5)))]
+    ml = max(len(p) for p in ps) + 1 + int(rng.integers(8, 24))
+    spec = bool(rng.integers(0, 2))
+    res = run_group(tp, PT.model_task, (cfg, 11, ps, ml, spec, dict(SSM_CFG, vocab_size=V)),
+                    env={"FFMI_TP_OVERLAP": str(int(rng.integers(0, 2)))}, max_bytes=1 << 20)
+    for r in range(1, tp):
+        assert res[r] == res[0], (cfg, tp, spec)
+    for p, toks in zip(ps, res[0]):
+        assert len(toks) == ml
+        check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp, max_tie_frac=0.1)
+
+
 @pytest.mark.parametrize("queues", ["1", None], ids=["one_queue", "hip_default_queues"])
 def test_peer_tp2_spec_infer_equals_incr(queues):
     """SpecInfer over the transport: identical to incremental decoding of the
