@@ -11,7 +11,9 @@ through the MI355X path:
     first run: 5 ties in 4281 tokens, at most 2 in one sequence);
   * SpecInfer with 1-2 random SSMs (the multi-SSM merge under
     FFMI_SPEC_EXT_MULTI_SSM) and random tree widths up to 4: its tokens under
-    the same rule -- so SpecInfer equals incremental decoding up to ties.
+    the same rule -- so SpecInfer equals incremental decoding up to ties;
+  * the full-precision path (fp32, incr or SpecInfer): equal to the fp32
+    oracle's free-running greedy decode up to fp32-level ties.
 """
 import numpy as np
 import pytest
@@ -109,3 +111,74 @@ def test_random_model_spec_infer_vs_oracle(seed):
         for s in ssms:
             s.close()
     check_all(cfg, 200 + seed, ps, res, ml, (cfg, B, mtb, widths, nssm))
+
+
+def oracle_free_running(cfg, seed, prompt, max_length):
+    """the fp32 oracle's own greedy continuation of one prompt (BOS
+    included) and its logit rows"""
+    import oracle_lib as O
+    om = O.Model(cfg, seed, fp16=0, max_requests=1, max_seq=max_length + 1)
+    seq = list(prompt)
+    last = om.forward_multi([0], [len(seq)], [0], np.array(seq, np.int32))[-1:]
+    rows = []
+    while len(seq) < max_length:
+        ids, _ = O.softmax_argmax(last, fp16=0)
+        rows.append(last[0])
+        seq.append(int(ids[0]))
+        if len(seq) < max_length:
+            last = om.decode_batch([0], [seq[-1]], [len(seq) - 1])
+    return seq, rows
+
+
+@pytest.mark.parametrize("seed", range(10))
+def test_random_model_full_precision_vs_oracle(seed):
+    """The full-precision path (fp32 end to end, the reference's
+    --use-full-precision where its exact-diff bars live) at random shapes:
+    incremental decoding and SpecInfer (fp32 SSMs, widths up to 4, 1-2 SSMs)
+    equal to the fp32 oracle's free-running greedy decode, a divergence
+    accepted only at an fp32-level tie (oracle gap <= 1e-4,
+    test_gpu_full_precision's rule)."""
+    rng = np.random.default_rng(9900 + seed)
+    cfg = random_cfg(rng)
+    V = cfg["vocab_size"]
+    ps, ml = random_requests(rng, V)
+    B = int(rng.choice([1, 2, 4, 8]))
+    mtb = int(rng.choice([32, 64, 128]))
+    spec = bool(rng.integers(0, 2))
+    kw = dict(max_requests=B, max_seq_len=128, full_precision=True)
+    ssms = []
+    if spec:
+        widths = WIDTHS[int(rng.integers(0, len(WIDTHS)))]
+        nssm = int(rng.integers(1, 3))
+        tree = 64 if nssm > 1 else 33
+        ext = fa.ffmi.SPEC_EXT_WIDTH4 | (fa.ffmi.SPEC_EXT_MULTI_SSM if nssm > 1 else 0)
+        vt = mtb + tree * B
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=128, spec_tree_width=widths,
+                               max_spec_tree_token_num=tree, spec_extensions=ext)
+        m = fa.Model(cfg, "tree", max_tokens=vt, max_tree_tokens=tree, weight_seed=400 + seed, **kw)
+        for k in range(nssm):
+            ssms.append(fa.Model(random_cfg(rng, vocab=V), "beam", max_tokens=vt,
+                                 max_tree_tokens=tree, weight_seed=500 + k, **kw))
+            rm.register_ssm_model(ssms[-1])
+    else:
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=128)
+        m = fa.Model(cfg, "inc", max_tokens=mtb, weight_seed=400 + seed, **kw)
+    try:
+        res = fa.generate(rm, m, ps, max_length=ml, spec=spec)
+    except fa.ffmi.FFMIError as e:
+        assert spec and "SSM loaded less" in str(e)
+        pytest.skip("SSM prompt behind the LLM for this random mix")
+    finally:
+        m.close()
+        for s in ssms:
+            s.close()
+    for p, r in zip(ps, res):
+        ref, rows = oracle_free_running(cfg, 400 + seed, [1] + list(p), ml)
+        g = r.output_tokens
+        assert len(g) == ml
+        if g != ref:
+            t = next(i for i in range(ml) if g[i] != ref[i])
+            row = rows[t - (len(p) + 1)]
+            assert float(row[ref[t]] - row[g[t]]) <= 1e-4, (t, cfg, spec)
