@@ -845,6 +845,38 @@ def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
     c.check(np.stack(got), np.stack(want))
 
 
+@pytest.mark.parametrize("d", [64, 128])
+def test_attention_long_context_vs_oracle(d):
+    """Long contexts (up to ~3000 keys: ~95 32-key chunks, many per wave):
+    a chunked prefill of 3 requests (1024-token steps, requests interleaved;
+    48 sampled rows per step) and a decode step at that depth, against the
+    oracle."""
+    rng = np.random.default_rng(31 + d)
+    R = 3
+    c = AttnCase(F.ATTN_INC, d=d, heads=2, max_requests=R, max_seq=3200, tree=64, max_tokens=1024)
+    plen = {r: int(rng.integers(900, 3000)) for r in range(R)}
+    got, want = [], []
+    done = {r: 0 for r in range(R)}
+    while any(done[r] < plen[r] for r in range(R)):  # 1024-token chunks, requests interleaved
+        infos, budget = [], 1024
+        for r in range(R):
+            n = min(plen[r] - done[r], budget)
+            infos += [(3, p, r, p, p + 1, 0, 0, 0) for p in range(done[r], done[r] + n)]
+            done[r] += n
+            budget -= n
+        out, qs = c.run(infos, rng=rng)
+        for t in rng.choice(len(infos), size=min(48, len(infos)), replace=False):  # sampled rows
+            i = infos[t]
+            got.append(out[t])
+            want.append(c.ref_row(qs[t], i[2], range(i[1] + 1)))
+    infos = [(7, plen[r], r, plen[r], plen[r] + 1, 0, 0, 0) for r in range(R)]
+    out, qs = c.run(infos, rng=rng)
+    for t, i in enumerate(infos):
+        got.append(out[t])
+        want.append(c.ref_row(qs[t], i[2], range(i[1] + 1)))
+    c.check(np.stack(got), np.stack(want))
+
+
 @pytest.mark.parametrize("seed", range(8))
 def test_attention_spec_random_beam_trees_vs_oracle(seed):
     """SSM beam steps at random shapes (the 68M SSM's d = 64): 1-4 requests

@@ -182,3 +182,25 @@ def test_random_model_full_precision_vs_oracle(seed):
             t = next(i for i in range(ml) if g[i] != ref[i])
             row = rows[t - (len(p) + 1)]
             assert float(row[ref[t]] - row[g[t]]) <= 1e-4, (t, cfg, spec)
+
+
+@pytest.mark.parametrize("seed", range(2))
+def test_random_model_long_context_vs_oracle(seed):
+    """Long contexts through the model: max_sequence_length 1024, prompts of
+    300-900 tokens loaded in 256-token chunks next to decoding requests, 16
+    new tokens each (incremental decoding), every pick teacher-forced through
+    the oracle under the tie rule."""
+    rng = np.random.default_rng(9700 + seed)
+    cfg = random_cfg(rng)
+    V = cfg["vocab_size"]
+    ps = [rng.integers(3, V, size=int(rng.integers(300, 900))).tolist() for _ in range(3)]
+    ml = max(len(p) for p in ps) + 17
+    rm = fa.RequestManager(max_requests_per_batch=3, max_tokens_per_batch=256,
+                           max_sequence_length=1024)
+    m = fa.Model(cfg, "inc", max_requests=3, max_tokens=256, max_seq_len=1024,
+                 weight_seed=700 + seed)
+    try:
+        res = fa.generate(rm, m, ps, max_length=ml)
+    finally:
+        m.close()
+    check_all(cfg, 700 + seed, ps, res, ml, (cfg, "long"))
