@@ -280,7 +280,12 @@ static void rope_table(std::vector<float> &tab, int max_pos, int d, const ffmi_a
 
 extern "C" ffmi_status ffmi_attn_create(const ffmi_attn_cfg *cfg, ffmi_attn **out) {
   FFMI_CHECK(cfg && out, FFMI_ERR_INVALID);
-  FFMI_CHECK(cfg->head_dim == 64 || cfg->head_dim == 128, FFMI_ERR_UNSUPPORTED);
+  // head sizes of the reference's kernels: 32 / 64 / 128 for incremental
+  // decoding (inc_multihead_self_attention.cu:911-926), 64 / 128 for tree
+  // verification and beam search (tree_inc...cu:562-572, spec_inc...cu:431-441)
+  FFMI_CHECK(cfg->head_dim == 64 || cfg->head_dim == 128 ||
+                 (cfg->head_dim == 32 && cfg->mode == FFMI_ATTN_INC),
+             FFMI_ERR_UNSUPPORTED);
   FFMI_CHECK(cfg->num_heads > 0 && cfg->max_requests > 0 && cfg->max_seq_len > 0 &&
                  cfg->max_tokens > 0,
              FFMI_ERR_INVALID);

@@ -342,6 +342,10 @@ hipError_t launch_kv_update(const char *blob, int T, int W, int C, const uint16_
     hipLaunchKernelGGL(kv_update_kernel<64>, grid, dim3(FFMI_ATTN_QTILE * 8), 0, s, blob, T, W, C, qkv, pp,
                        qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
                        max_rope_pos);
+  else if (d == 32)  // (incremental decoding only: ffmi_attn_create)
+    hipLaunchKernelGGL(kv_update_kernel<32>, grid, dim3(FFMI_ATTN_QTILE * 4), 0, s, blob, T, W, C, qkv, pp,
+                       qkvp.S, qkvp.NP, qbuf, kc, vc, stage_wr, stage_rd, rope, heads, slots,
+                       max_rope_pos);
   else
     return hipErrorInvalidValue;
   return hipGetLastError();
@@ -1012,6 +1016,9 @@ hipError_t launch_attention(const char *blob, int W, int max_q, uint16_t *qbuf, 
                                    fused, kv);
   if (d == 64)
     return launch_attention_d<64>(blob, W, max_q, qbuf, kc, vc, out, heads, slots, scale, s, op,
+                                  fused, kv);
+  if (d == 32)  // incremental decoding's third head size (inc...cu:911-926)
+    return launch_attention_d<32>(blob, W, max_q, qbuf, kc, vc, out, heads, slots, scale, s, op,
                                   fused, kv);
   return hipErrorInvalidValue;
 }

@@ -393,7 +393,7 @@ hipError_t launch_attention_f32(const char *blob, int T, const float *qbuf, cons
                                 float scale, hipStream_t s) {
   if (T <= 0) return hipSuccess;
   const size_t lds = (size_t)(d + 256 + slots) * sizeof(float);
-  if (lds > 64 * 1024 || (d != 64 && d != 128)) return hipErrorInvalidValue;
+  if (lds > 64 * 1024 || (d != 32 && d != 64 && d != 128)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(f32_attention_kernel, dim3(T, heads), dim3(256), lds, s, blob, qbuf, kc, vc,
                      out, heads, d, slots, scale);
   return hipGetLastError();

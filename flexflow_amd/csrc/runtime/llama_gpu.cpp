@@ -403,7 +403,8 @@ struct LlamaGPU : public ffmi_model {
                FFMI_ERR_UNSUPPORTED);
     FFMI_CHECK(H % c.num_heads == 0 && c.num_heads % P == 0 && F % P == 0, FFMI_ERR_INVALID);
     d = H / c.num_heads;
-    FFMI_CHECK(d == 64 || d == 128, FFMI_ERR_UNSUPPORTED);
+    // (d = 32: incremental decoding only, as the reference's kernels)
+    FFMI_CHECK(d == 64 || d == 128 || (d == 32 && mode == FFMI_MODEL_INC), FFMI_ERR_UNSUPPORTED);
     heads_l = c.num_heads / P;
     Hl = heads_l * d;
     Fl = F / P;

@@ -57,6 +57,12 @@ def test_invalid_arguments_return_status_not_abort():
     cfg = F.AttnCfg(0, 2, 96, 1, 16, 0, 16, 0.1, 10000.0, 0)  # head_dim 96 unsupported
     h = ctypes.c_void_p()
     assert L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(h)) == 5
+    # head_dim 32: incremental decoding only, as the reference's kernels
+    # (inc...cu:911-926 take 32 / 64 / 128; tree_inc...cu:562-572 and
+    # spec_inc...cu:431-441 64 / 128)
+    for mode in (F.ATTN_TREE, F.ATTN_SPEC):
+        cfg = F.AttnCfg(mode, 2, 32, 1, 16, 8, 16, 0.1, 10000.0, 0)
+        assert L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(h)) == 5
 
 
 def test_full_precision_model_opts_and_no_device():

@@ -616,7 +616,7 @@ class AttnCase:
 
 
 @pytest.mark.parametrize("layout,fp32", [(0, False), (1, False), (0, True)])
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128])
 def test_attention_inc_prefill_then_decode(d, layout, fp32):
     rng = np.random.default_rng(d)
     c = AttnCase(F.ATTN_INC, d=d, out_layout=layout, fp32=fp32)
@@ -624,16 +624,17 @@ def test_attention_inc_prefill_then_decode(d, layout, fp32):
     lens = {0: 20, 1: 37, 2: 10}
     infos = [(5, p, r, p, p + 1, 0, 0, 0) for r, n in lens.items() for p in range(n)]
     out, qs = c.run(infos, rng=rng)
-    for t, i in enumerate(infos):
-        c.check(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)))
+    got = [out[t] for t in range(len(infos))]
+    want = [c.ref_row(qs[t], i[2], range(i[1] + 1)) for t, i in enumerate(infos)]
     infos = [(7, 20, 0, 20, 21, 0, 0, 0), (7, 37, 1, 37, 38, 0, 0, 0)] + \
             [(7, p, 2, p, p + 1, 0, 0, 0) for p in range(10, 15)]
     out, qs = c.run(infos, rng=rng)
-    for t, i in enumerate(infos):
-        c.check(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)))
+    got += [out[t] for t in range(len(infos))]
+    want += [c.ref_row(qs[t], i[2], range(i[1] + 1)) for t, i in enumerate(infos)]
+    c.check(np.stack(got), np.stack(want))  # (the exact-fraction bar over all rows)
 
 
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128])
 def test_attention_llama3_rope_scaling(d):
     """llama3 frequency scaling (inc_multihead_self_attention.cu:703-722) in
     the handle's RoPE table: original_max_position 64 puts the three
@@ -643,11 +644,12 @@ def test_attention_llama3_rope_scaling(d):
     lens = {0: 33, 1: 57}
     infos = [(5, p, r, p, p + 1, 0, 0, 0) for r, n in lens.items() for p in range(n)]
     out, qs = c.run(infos, rng=rng)
-    for t, i in enumerate(infos):
-        close16(out[t], c.ref_row(qs[t], i[2], range(i[1] + 1)), exact_frac=0.98)
+    # (the exact-fraction bar over all rows: a d = 32 row has only 64 values)
+    close16(out[:len(infos)], np.stack([c.ref_row(qs[t], i[2], range(i[1] + 1))
+                                        for t, i in enumerate(infos)]), exact_frac=0.98)
 
 
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128])
 def test_attention_fused_equals_two_launch_path(d, monkeypatch):
     """One workgroup per request (decode / beam / verify steps) runs commits,
     KV update and attention in one launch; FFMI_ATTN_NO_FUSE=1 runs the
@@ -845,7 +847,7 @@ def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
     c.check(np.stack(got), np.stack(want))
 
 
-@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("d", [32, 64, 128])
 def test_attention_long_context_vs_oracle(d):
     """Long contexts (up to ~3000 keys: ~95 32-key chunks, many per wave):
     a chunked prefill of 3 requests (1024-token steps, requests interleaved;

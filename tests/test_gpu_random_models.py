@@ -1,5 +1,5 @@
 """Randomised end-to-end GPU parity: small LLaMA models of random shape
-(1-3 layers, 1-8 heads of d = 64 or 128, random FFN width and vocabulary,
+(1-3 layers, 1-8 heads of d = 64 or 128, and 32 in incremental decoding, random FFN width and vocabulary,
 RoPE theta, RMS eps), random scheduler limits (batch slots, token budget) and
 random request mixes (1-10 prompts of 1-60 tokens, queued past the slots),
 through the MI355X path:
@@ -38,9 +38,11 @@ pytestmark = pytest.mark.gpu
 WIDTHS = [(1, 1, 3), (3,), (2, 1, 1), (1, 1, 4), (2, 2), ()]
 
 
-def random_cfg(rng, vocab=None):
+def random_cfg(rng, vocab=None, inc=False):
+    """inc: incremental decoding only, where d = 32 is a third head size (the
+    reference's inc kernels take 32 / 64 / 128, tree and beam 64 / 128)"""
     heads = int(rng.choice([1, 2, 4, 8]))
-    d = int(rng.choice([64, 128]))
+    d = int(rng.choice([32, 64, 128] if inc else [64, 128]))
     return dict(num_layers=int(rng.integers(1, 4)),
                 vocab_size=int(vocab or rng.integers(100, 5000)),
                 num_heads=heads, num_kv_heads=heads, hidden=heads * d,
@@ -59,7 +61,7 @@ def random_requests(rng, V):
 @pytest.mark.parametrize("seed", range(20))
 def test_random_model_incr_decoding_vs_oracle(seed):
     rng = np.random.default_rng(9000 + seed)
-    cfg = random_cfg(rng)
+    cfg = random_cfg(rng, inc=True)
     ps, ml = random_requests(rng, cfg["vocab_size"])
     B = int(rng.choice([1, 2, 3, 4, 8]))
     mtb = int(rng.choice([8, 16, 32, 64, 128]))
