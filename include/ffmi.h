@@ -111,7 +111,7 @@ ffmi_status ffmi_batch_upload(ffmi_batch_dev *b, const ffmi_batch_desc *desc,
 typedef struct {
   int mode;            /* ffmi_attn_mode                                     */
   int num_heads;       /* heads on this shard                                */
-  int head_dim;        /* 64 or 128                                          */
+  int head_dim;        /* 64 or 128; 32 too in FFMI_ATTN_INC (inc...cu:911) */
   int max_requests;    /* KV rows                                            */
   int max_seq_len;     /* committed slots per request (S)                    */
   int max_tree_tokens; /* extra slots for tree / spec (S' = S + tree)        */
