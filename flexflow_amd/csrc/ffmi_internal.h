@@ -11,6 +11,7 @@
     hipError_t e_ = (expr);                              \
     if (e_ != hipSuccess) {                              \
       ffmi_set_last_error(hipGetErrorString(e_), __FILE__, __LINE__); \
+      (void)hipGetLastError(); /* reset: no stale error for a later launch check */ \
       return FFMI_ERR_HIP;                               \
     }                                                    \
   } while (0)

@@ -202,7 +202,7 @@ struct LlamaF32 : public ffmi_model {
     // weights: full tensors through a staging buffer, this shard's rows /
     // columns copied out
     float *tmp = nullptr;
-    TRY(alloc(&tmp, std::max((size_t)V * H, (size_t)F * H)));
+    TRY(alloc(&tmp, std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H))));
     const bool synth = weights_folder.empty();
     const bool chain = o.weight_init == 2 && synth;
     const int kres = o.weight_init == 1 ? (FFMI_WKIND_DEPTH | c.num_layers) : 0;

@@ -1,41 +1,65 @@
 """Randomised end-to-end GPU parity: small LLaMA models of random shape
-(1-3 layers, 1-8 heads of d = 64 or 128, and 32 in incremental decoding, random FFN width and vocabulary,
+(1-3 layers, 1-8 heads of d = 64 or 128 -- and 32 in incremental decoding --
+random FFN width and vocabulary,
 RoPE theta, RMS eps), random scheduler limits (batch slots, token budget) and
 random request mixes (1-10 prompts of 1-60 tokens, queued past the slots),
 through the MI355X path:
 
   * incremental decoding: every request's tokens teacher-forced through the
-    oracle, under test_gpu_e2e's tie rule (a mismatch must be a tie of the
-    two tokens' fp16 probabilities within 2 ulp), with the ties of a test
-    capped at max(2, 3%) of its picks (the tie cap of tests/parity_rules.py;
-    first run: 5 ties in 4281 tokens, at most 2 in one sequence);
+    oracle under the tie rule of tests/parity_rules.py (a mismatch must be a
+    <= 2-ulp probability tie or an oracle logit gap within 3 sigma_pair of
+    the row's fp32-reordering noise), the ties of a test capped at max(2, 3%)
+    of its picks (first run: 5 ties in 4281 picks; a 150-seed sweep found
+    3-7-ulp ties that only the sigma_pair part admits);
   * SpecInfer with 1-2 random SSMs (the multi-SSM merge under
     FFMI_SPEC_EXT_MULTI_SSM) and random tree widths up to 4: its tokens under
     the same rule -- so SpecInfer equals incremental decoding up to ties;
   * the full-precision path (fp32, incr or SpecInfer): equal to the fp32
     oracle's free-running greedy decode up to fp32-level ties.
 """
+import os
+
 import numpy as np
 import pytest
 
 import flexflow_amd as fa
-from test_gpu_e2e import check_tokens_vs_oracle
-
-
-def check_all(cfg, seed, ps, res, ml, what):
-    """every request under the tie rule; the test's ties capped at max(2, 3%)"""
-    ties = total = 0
-    for p, r in zip(ps, res):
-        assert len(r.output_tokens) == ml, what
-        n = len(r.output_tokens) - (len(p) + 1)
-        ties += n - check_tokens_vs_oracle(cfg, seed, r.output_tokens, len(p) + 1,
-                                           max_tie_frac=1.0)
-        total += n
-    assert ties <= max(2, 0.03 * total), (ties, total, what)
+from hip_util import report
 
 pytestmark = pytest.mark.gpu
 
 WIDTHS = [(1, 1, 3), (3,), (2, 1, 1), (1, 1, 4), (2, 2), ()]
+# FFMI_RANDOM_SEEDS: more seeds for a one-off sweep (the suite runs 20 / 10)
+SEEDS = int(os.environ.get("FFMI_RANDOM_SEEDS", "20"))
+
+
+def check_all(cfg, seed, ps, res, ml, what):
+    """every request teacher-forced through the oracle under the one tie rule
+    of tests/parity_rules.py (a mismatch must be a <= 2-ulp probability tie
+    or an oracle logit gap within 3 sigma_pair of the row's fp32-reordering
+    noise, the oracle re-run with its dots reordered), and the test's ties
+    capped at max(2, 3%) of its picks"""
+    import oracle_lib as O
+    from parity_rules import assert_ties, classify, picks
+    verdicts, total = [], 0
+    for p, r in zip(ps, res):
+        seq = r.output_tokens
+        assert len(seq) == ml, what
+        n0 = len(p) + 1
+        m = O.Model(cfg, seed, fp16=1, max_requests=1, max_seq=len(seq) + 1)
+        z0 = m.forward(0, np.array(seq[:-1], np.int32), 0)[n0 - 1:]
+        gen, o = seq[n0:], picks(z0)
+        mism = [t for t in range(len(gen)) if o[t] != gen[t]]
+        if mism:
+            O.set_dot_variant(1)
+            try:
+                m1 = O.Model(cfg, seed, fp16=1, max_requests=1, max_seq=len(seq) + 1)
+                z1 = m1.forward(0, np.array(seq[:-1], np.int32), 0)[n0 - 1:]
+            finally:
+                O.set_dot_variant(0)
+            verdicts += [dict(classify(z0[t], z1[t], gen[t], o[t]), pos=t) for t in mism]
+        total += len(gen)
+    report("random_model_ties", where=str(what)[:120], ties=len(verdicts), total=total)
+    assert_ties(verdicts, total)
 
 
 def random_cfg(rng, vocab=None, inc=False):
@@ -58,7 +82,7 @@ def random_requests(rng, V):
     return ps, max_length
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(SEEDS))
 def test_random_model_incr_decoding_vs_oracle(seed):
     rng = np.random.default_rng(9000 + seed)
     cfg = random_cfg(rng, inc=True)
@@ -76,7 +100,7 @@ def test_random_model_incr_decoding_vs_oracle(seed):
     check_all(cfg, 100 + seed, ps, res, ml, (cfg, B, mtb))
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(SEEDS))
 def test_random_model_spec_infer_vs_oracle(seed):
     rng = np.random.default_rng(9500 + seed)
     cfg = random_cfg(rng)
@@ -132,7 +156,7 @@ def oracle_free_running(cfg, seed, prompt, max_length):
     return seq, rows
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(max(1, SEEDS // 2)))
 def test_random_model_full_precision_vs_oracle(seed):
     """The full-precision path (fp32 end to end, the reference's
     --use-full-precision where its exact-diff bars live) at random shapes:
