@@ -373,15 +373,17 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     for (int j = 0; j < 4; ++j)
       if (j == k - 1) L = top[j];
   }
-  // the sum uses the hardware exp2 (__expf, a few ulp): over 32000 terms
-  // accumulated in double its error stays orders of magnitude below the
-  // float rounding of S; the p values that are compared use the accurate expf
+  // the sum's terms use the accurate expf, as the p values and the oracle
+  // do: with the hardware exp2 (__expf, a few ulp) a peaked row, whose S a few
+  // terms dominate, took their errors straight into S's float rounding, and
+  // 1 p in ~10^4 came out one fp16 ulp off (the random-shape sweep of
+  // test_softmax_topk_random_shapes_exact)
   double se = 0.0;
 #pragma unroll
   for (int v = 0; v < NV; ++v)
     if (v * TPB + tid < nvec)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) se += (double)__expf(elem(v, e) - M);
+      for (int e = 0; e < 8; ++e) se += (double)expf(elem(v, e) - M);
   se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
@@ -525,7 +527,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
       if (j == k - 1) L = top[j];
   }
   double se = 0.0;
-  for (int i = tid; i < V; i += TPB) se += (double)__expf(h2f_(x[i]) - M);
+  for (int i = tid; i < V; i += TPB) se += (double)expf(h2f_(x[i]) - M);
   se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
@@ -711,7 +713,7 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
     // (exchange buffer: [P][T][W] of phase 0 is read above and rewritten
     //  below only after the whole block has read it)
     double se = 0.0;
-    for (int i = tid; i < Vl; i += TPB) se += (double)__expf(h2f_(x[i]) - M);
+    for (int i = tid; i < Vl; i += TPB) se += (double)expf(h2f_(x[i]) - M);
     se = __ockl_wfred_add_f64(se);
     if (lane == 0) dsh[wv] = se;
     __syncthreads();

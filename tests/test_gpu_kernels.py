@@ -7,6 +7,7 @@ elements bit-identical; norms within 1 ulp; argmax / top-k / embedding /
 weights bit-exact.
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -16,6 +17,8 @@ import oracle_lib as O
 from hip_util import Buf, f16, hip, ulp_diff
 
 pytestmark = pytest.mark.gpu
+# FFMI_RANDOM_SCALE: k times the seeds of the random-shape tests (one-off sweeps)
+RS = int(os.environ.get("FFMI_RANDOM_SCALE", "1"))
 
 L = None
 
@@ -192,7 +195,7 @@ def test_linear_gate_up_silu_fused(T):
     close16(Yb.get(), ref, max_ulp=3, exact_frac=0.99, atol=1e-3)
 
 
-@pytest.mark.parametrize("seed", range(20))
+@pytest.mark.parametrize("seed", range(20 * RS))
 def test_linear_random_shapes_vs_oracle(seed):
     """ffmi_linear at random shapes against the oracle: T 1-1100 (skinny,
     wave, M-split with 2-4 row tiles per wave and split K, the 256 x 256 tile
@@ -396,7 +399,7 @@ def test_softmax_argmax_topk_exact(V):
         np.testing.assert_array_equal(pr.get(), rp)
 
 
-@pytest.mark.parametrize("seed", range(10))
+@pytest.mark.parametrize("seed", range(10 * RS))
 def test_softmax_topk_random_shapes_exact(seed):
     """Softmax + argmax / top-k (k 1-4) at random shapes, bit-exact against
     the oracle: T 1-300, V from 64 to 140000 (multiples of 8 take the
@@ -420,7 +423,7 @@ def test_softmax_topk_random_shapes_exact(seed):
     np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(8 * RS))
 def test_rmsnorm_random_shapes(seed):
     """RMSNorm / residual RMSNorm at random T (1-1100) and H (multiple of 8
     up to 16384): residual bit-exact, output within 1 fp16 ulp of the
@@ -787,7 +790,7 @@ def random_layer_tree(rng, n, max_width=4):
 
 @pytest.mark.parametrize("path", ["default", "qsplit", "two_launch"])
 @pytest.mark.parametrize("d", [64, 128])
-@pytest.mark.parametrize("seed", range(6))
+@pytest.mark.parametrize("seed", range(6 * RS))
 def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
     """Tree verification at random shapes against the oracle: 1-4 requests
     with random prompt lengths (crossing the 32-key chunks and the LDS tail),
@@ -879,7 +882,7 @@ def test_attention_long_context_vs_oracle(d):
     c.check(np.stack(got), np.stack(want))
 
 
-@pytest.mark.parametrize("seed", range(8))
+@pytest.mark.parametrize("seed", range(8 * RS))
 def test_attention_spec_random_beam_trees_vs_oracle(seed):
     """SSM beam steps at random shapes (the 68M SSM's d = 64): 1-4 requests
     with random prompts, then one step per tree layer -- the layer's nodes are
