@@ -48,7 +48,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     uint16_t *__restrict__ out, int H, float eps, int out_packed,
     const float *__restrict__ x2p, int pS, int pNP, const char *__restrict__ gather,
     uint4 *__restrict__ blob_dst, int blob_n16) {
-  __shared__ float scratch[NT / 64];
+  __shared__ double scratch[NT / 64];
   const int row = blockIdx.x;
   const int T = gridDim.x;
   const int nchunk = H >> 3;
@@ -103,7 +103,11 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     if (S == 2 && MAXC > 1) xb[c] = fold();
   }
   if (S == 2 && MAXC == 1) xb[0] = fold();
-  float ss = 0.f;
+  // the sum of squares in fp64, as the oracle's (exact products, then one
+  // rounding to float): an fp32 sum in another order than the oracle's moved
+  // rms across a half rounding boundary in ~1 row in 10^3 at H = 16160
+  // (test_rmsnorm_random_shapes sweep), where every output of the row shifts
+  double ss = 0.0;
 #pragma unroll
   for (int c = 0; c < MAXC; ++c) {
     const int ch = threadIdx.x + c * NT;
@@ -119,7 +123,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
 #pragma unroll
           for (int q = 0; q < 8; ++q) {
             const float f = h2f_(ea[q]) + h2f_(eb[q]);
-            ss += f * f;
+            ss += (double)f * (double)f;
           }
         }
         __half2 r[4];
@@ -135,13 +139,13 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
       if (!FAULT) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
-          float f = h2f_(e[q]);
-          ss += f * f;
+          const float f = h2f_(e[q]);
+          ss += (double)f * (double)f;
         }
       }
     }
   }
-  const float sum = block_sum<NT / 64>(ss, scratch);
+  const float sum = (float)block_sum<NT / 64>(ss, scratch);
   // sqrtf: the correctly rounded square root (HIP's __fsqrt_rn is the native
   // v_sqrt_f32, ~1 ulp, unless OCML_BASIC_ROUNDED_OPERATIONS is defined)
   const float rms_f = __fdiv_rn(1.0f, sqrtf(__fadd_rn(__fdiv_rn(sum, (float)H), eps)));

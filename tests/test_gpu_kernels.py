@@ -240,7 +240,7 @@ def test_linear_random_shapes_vs_oracle(seed):
             g16, u16 = g.astype(np.float16), u.astype(np.float16)
             chain = lambda a, b: O.silu_mul(a.astype(np.float32), b.astype(np.float32))  # noqa: E731
             y16 = y.astype(np.float16)
-            assert (y16 == chain(g16, u16).astype(np.float16)).mean() >= 0.98
+            assert (y16 == chain(g16, u16).astype(np.float16)).mean() >= min(0.98, 1 - 2 / y.size)
             sp = lambda a: np.spacing(np.abs(a).astype(np.float16)).astype(np.float32)  # noqa: E731
             dg = np.maximum(2 * sp(g16), 1e-4 * np.abs(g).max())
             du = np.maximum(2 * sp(u16), 1e-4 * np.abs(u).max())
@@ -249,8 +249,9 @@ def test_linear_random_shapes_vs_oracle(seed):
             slack = sp(np.maximum(np.abs(lo), np.abs(hi)))
             yf = y16.astype(np.float32)
             assert not ((yf < lo - slack) | (yf > hi + slack)).any(), (T, N, K, flags)
-        else:
-            close16(y, O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1))
+        else:  # (>= 99% bit-identical, or all but two elements of a tiny output)
+            close16(y, O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1),
+                    exact_frac=min(0.99, 1.0 - 2.0 / y.size))
 
 
 @pytest.mark.parametrize("Ts", [(1, 8, 40, 64), (65, 100, 168, 192)])
