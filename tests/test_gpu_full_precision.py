@@ -16,6 +16,8 @@ if it ever happens).
 """
 import ctypes
 
+import os
+
 import numpy as np
 import pytest
 
@@ -58,6 +60,29 @@ def test_linear_f32_against_fp64(T, N, K):
     err = np.abs(y1 - ref)
     assert np.all(err <= 2e-6 * mag + 1e-30), float((err / mag).max())
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
+
+
+@pytest.mark.parametrize("seed", range(12 * int(os.environ.get("FFMI_RANDOM_SCALE", "1"))))
+def test_linear_f32_random_shapes(seed):
+    """ffmi_linear_f32 at random shapes (T 1-1100, N 1-6000 ragged, K a
+    multiple of 32 up to 8192) under the same bound and determinism as
+    test_linear_f32_against_fp64."""
+    rng = np.random.default_rng(8800 + seed)
+    T = int(np.exp(rng.uniform(0, np.log(1100))))
+    N = int(rng.integers(1, 6000))
+    K = 32 * int(np.exp(rng.uniform(0, np.log(256))))
+    X = rng.uniform(-1, 1, (T, K)).astype(np.float32)
+    W = rng.uniform(-1, 1, (N, K)).astype(np.float32)
+    ref = X.astype(np.float64) @ W.astype(np.float64).T
+    mag = np.abs(X).astype(np.float64) @ np.abs(W).astype(np.float64).T
+    bx, bw, by = Buf(X), Buf(W), Buf.empty((T, N), np.float32)
+    L = F.lib()
+    assert L.ffmi_linear_f32(bx.ptr, bw.ptr, by.ptr, T, N, K, None) == 0, (T, N, K)
+    y1 = by.get()
+    assert L.ffmi_linear_f32(bx.ptr, bw.ptr, by.ptr, T, N, K, None) == 0
+    err = np.abs(y1 - ref)
+    assert np.all(err <= 2e-6 * mag + 1e-30), (T, N, K, float((err / mag).max()))
+    assert np.array_equal(y1.view(np.uint32), by.get().view(np.uint32))
 
 
 def ulps32(a, b):
