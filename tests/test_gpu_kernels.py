@@ -793,6 +793,19 @@ def random_layer_tree(rng, n, max_width=4):
 @pytest.mark.parametrize("d", [64, 128])
 @pytest.mark.parametrize("seed", range(6 * RS))
 def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
+    _random_tree_case(d, seed, path, monkeypatch, fp32=False)
+
+
+@pytest.mark.parametrize("d", [64, 128])
+@pytest.mark.parametrize("seed", range(4 * RS))
+def test_attention_f32_random_trees_vs_oracle(d, seed, monkeypatch):
+    """the DT_FLOAT attention handle (fp32 caches, --use-full-precision) on
+    the same random trees, prefixes and commits: every row within 2e-6 of
+    the oracle's fp32 attention"""
+    _random_tree_case(d, seed, "default", monkeypatch, fp32=True)
+
+
+def _random_tree_case(d, seed, path, monkeypatch, fp32):
     """Tree verification at random shapes against the oracle: 1-4 requests
     with random prompt lengths (crossing the 32-key chunks and the LDS tail),
     random layer-order trees of 1-64 nodes (the merged multi-SSM bound: mask
@@ -808,7 +821,8 @@ def test_attention_tree_random_trees_vs_oracle(d, seed, path, monkeypatch):
         monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
     rng = np.random.default_rng(1000 + 10 * d + seed)
     R = int(rng.integers(1, 5))
-    c = AttnCase(F.ATTN_TREE, d=d, max_requests=4, max_seq=200, tree=64, max_tokens=512)
+    c = AttnCase(F.ATTN_TREE, d=d, max_requests=4, max_seq=200, tree=64, max_tokens=512,
+                 fp32=fp32)
     plen = {r: int(rng.integers(1, 100)) for r in range(R)}
     infos = [(3, p, r, p, p + 1, 0, 0, 0) for r in range(R) for p in range(plen[r])]
     out, qs = c.run(infos, masks=[[0]] * R, rng=rng)
