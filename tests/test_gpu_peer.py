@@ -121,6 +121,34 @@ def test_peer_tp_random_models(seed):
         check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp, max_tie_frac=0.1)
 
 
+@pytest.mark.parametrize("seed", range(4 * int(os.environ.get("FFMI_RANDOM_SCALE", "1"))))
+def test_peer_tp_random_models_spec_extensions(seed):
+    """TP 2 or 4 rank processes running the flagged extensions (tree width 4,
+    four merged SSMs; tests/spec_configs.py) at random small LLaMA shapes:
+    every rank emits the same tokens, oracle-valid picks of the UNSHARDED
+    model under the TP tie rule."""
+    from test_gpu_e2e import SSM_CFG, check_tokens_vs_oracle
+    rng = np.random.default_rng(4300 + seed)
+    tp = int(rng.choice([2, 4]))
+    heads = tp * int(rng.integers(1, 3))
+    d = int(rng.choice([64, 128]))
+    V = int(16 * tp * int(rng.integers(8, 60)))
+    cfg = dict(num_layers=int(rng.integers(1, 3)), vocab_size=V, num_heads=heads,
+               num_kv_heads=heads, hidden=heads * d, intermediate=32 * tp * int(rng.integers(1, 12)),
+               rms_eps=1e-6, rope_theta=10000.0)
+    ps = [rng.integers(3, V, size=int(rng.integers(2, 40))).tolist()
+          for _ in range(int(rng.integers(1, 5)))]
+    ml = max(len(p) for p in ps) + 1 + int(rng.integers(8, 24))
+    spec = ["w114", "ssm4"][seed % 2]
+    res = run_group(tp, PT.tp_generate_task,
+                    (cfg, 11, ps, ml, spec, dict(SSM_CFG, vocab_size=V)), max_bytes=2 << 20)
+    for r in range(1, tp):
+        assert res[r]["tokens"] == res[0]["tokens"], (cfg, tp, spec)
+    for p, toks in zip(ps, res[0]["tokens"]):
+        assert len(toks) == ml
+        check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp, max_tie_frac=0.1)
+
+
 @pytest.mark.parametrize("queues", ["1", None], ids=["one_queue", "hip_default_queues"])
 def test_peer_tp2_spec_infer_equals_incr(queues):
     """SpecInfer over the transport: identical to incremental decoding of the
