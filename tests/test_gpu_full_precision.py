@@ -62,12 +62,15 @@ def test_linear_f32_against_fp64(T, N, K):
     assert np.array_equal(y1.view(np.uint32), y2.view(np.uint32))
 
 
+OFF = int(os.environ.get("FFMI_RANDOM_SEED_OFFSET", "0"))  # fresh seeds for one-off sweeps
+
+
 @pytest.mark.parametrize("seed", range(12 * int(os.environ.get("FFMI_RANDOM_SCALE", "1"))))
 def test_linear_f32_random_shapes(seed):
     """ffmi_linear_f32 at random shapes (T 1-1100, N 1-6000 ragged, K a
     multiple of 32 up to 8192) under the same bound and determinism as
     test_linear_f32_against_fp64."""
-    rng = np.random.default_rng(8800 + seed)
+    rng = np.random.default_rng(8800 + OFF + seed)
     T = int(np.exp(rng.uniform(0, np.log(1100))))
     N = int(rng.integers(1, 6000))
     K = 32 * int(np.exp(rng.uniform(0, np.log(256))))

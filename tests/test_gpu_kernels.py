@@ -19,6 +19,7 @@ from hip_util import Buf, f16, hip, ulp_diff
 pytestmark = pytest.mark.gpu
 # FFMI_RANDOM_SCALE: k times the seeds of the random-shape tests (one-off sweeps)
 RS = int(os.environ.get("FFMI_RANDOM_SCALE", "1"))
+OFF = int(os.environ.get("FFMI_RANDOM_SEED_OFFSET", "0"))  # fresh seeds for one-off sweeps
 
 L = None
 
@@ -202,7 +203,7 @@ def test_linear_random_shapes_vs_oracle(seed):
     form), N from 16 to 20000 (ragged: not a multiple of 16 or 32), K a
     multiple of 32 up to 8192, with and without the SiLU-mul epilogue, row-
     major or packed activations in and out, weight-stream hint on or off."""
-    rng = np.random.default_rng(4242 + seed)
+    rng = np.random.default_rng(4242 + OFF + seed)
     for _ in range(3):
         T = int(np.exp(rng.uniform(0, np.log(1100))))
         N = int(rng.choice([int(rng.integers(16, 400)), int(rng.integers(400, 6000)),
@@ -406,7 +407,7 @@ def test_softmax_topk_random_shapes_exact(seed):
     the oracle: T 1-300, V from 64 to 140000 (multiples of 8 take the
     register kernel, others and V > 32768 the streaming one), logit scales
     from flat (fp16 p collapses, many candidates) to peaked, planted ties."""
-    rng = np.random.default_rng(777 + seed)
+    rng = np.random.default_rng(777 + OFF + seed)
     T = int(rng.integers(1, 301))
     V = int(rng.choice([int(rng.integers(8, 4096)) * 8, int(rng.integers(64, 40000)),
                         32000, 32001, int(rng.integers(32769, 140000))]))
@@ -429,7 +430,7 @@ def test_rmsnorm_random_shapes(seed):
     """RMSNorm / residual RMSNorm at random T (1-1100) and H (multiple of 8
     up to 16384): residual bit-exact, output within 1 fp16 ulp of the
     oracle and >= 99% bit-identical."""
-    rng = np.random.default_rng(555 + seed)
+    rng = np.random.default_rng(555 + OFF + seed)
     T = int(np.exp(rng.uniform(0, np.log(1100))))
     H = 8 * int(rng.integers(1, 2049))
     x1 = f16(rng.standard_normal((T, H)) * float(rng.choice([0.01, 1.0, 30.0])))
@@ -819,7 +820,7 @@ def _random_tree_case(d, seed, path, monkeypatch, fp32):
         monkeypatch.setenv("FFMI_ATTN_QSPLIT", "2")
     elif path == "two_launch":
         monkeypatch.setenv("FFMI_ATTN_NO_FUSE", "1")
-    rng = np.random.default_rng(1000 + 10 * d + seed)
+    rng = np.random.default_rng(1000 + OFF + 10 * d + seed)
     R = int(rng.integers(1, 5))
     c = AttnCase(F.ATTN_TREE, d=d, max_requests=4, max_seq=200, tree=64, max_tokens=512,
                  fp32=fp32)
@@ -905,7 +906,7 @@ def test_attention_spec_random_beam_trees_vs_oracle(seed):
     layer-order trees of up to 64 nodes (widths up to 4, merged-tree sizes);
     every query row against O.attention_row over its prefix + ancestors
     (the exact-fraction bar over all rows of the test)."""
-    rng = np.random.default_rng(2000 + seed)
+    rng = np.random.default_rng(2000 + OFF + seed)
     R = int(rng.integers(1, 5))
     c = AttnCase(F.ATTN_SPEC, d=64, max_requests=4, max_seq=160, tree=64, max_tokens=512)
     plen = {r: int(rng.integers(1, 100)) for r in range(R)}
