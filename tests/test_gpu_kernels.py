@@ -196,6 +196,14 @@ def test_linear_gate_up_silu_fused(T):
     close16(Yb.get(), ref, max_ulp=3, exact_frac=0.99, atol=1e-3)
 
 
+def flip_bound(rate, n):
+    """least bit-identical fraction of n outputs whose fp32 sums, added in
+    another order than the oracle's, flip their fp16 rounding at up to `rate`
+    each: rate * n + 3 sigma of that count, and at least two flips (a
+    500-seed sweep met 3 flips in a 260-output decode row at K = 5120)"""
+    return 1.0 - max(2.0, rate * n + 3.0 * np.sqrt(rate * n)) / n
+
+
 @pytest.mark.parametrize("seed", range(20 * RS))
 def test_linear_random_shapes_vs_oracle(seed):
     """ffmi_linear at random shapes against the oracle: T 1-1100 (skinny,
@@ -241,7 +249,7 @@ def test_linear_random_shapes_vs_oracle(seed):
             g16, u16 = g.astype(np.float16), u.astype(np.float16)
             chain = lambda a, b: O.silu_mul(a.astype(np.float32), b.astype(np.float32))  # noqa: E731
             y16 = y.astype(np.float16)
-            assert (y16 == chain(g16, u16).astype(np.float16)).mean() >= min(0.98, 1 - 2 / y.size)
+            assert (y16 == chain(g16, u16).astype(np.float16)).mean() >= flip_bound(0.02, y.size)
             sp = lambda a: np.spacing(np.abs(a).astype(np.float16)).astype(np.float32)  # noqa: E731
             dg = np.maximum(2 * sp(g16), 1e-4 * np.abs(g).max())
             du = np.maximum(2 * sp(u16), 1e-4 * np.abs(u).max())
@@ -250,9 +258,9 @@ def test_linear_random_shapes_vs_oracle(seed):
             slack = sp(np.maximum(np.abs(lo), np.abs(hi)))
             yf = y16.astype(np.float32)
             assert not ((yf < lo - slack) | (yf > hi + slack)).any(), (T, N, K, flags)
-        else:  # (>= 99% bit-identical, or all but two elements of a tiny output)
+        else:  # (>= 99% bit-identical, with the binomial margin of a small output)
             close16(y, O.linear(X.astype(np.float32), W.astype(np.float32), fp16=1),
-                    exact_frac=min(0.99, 1.0 - 2.0 / y.size))
+                    exact_frac=flip_bound(0.01, y.size))
 
 
 @pytest.mark.parametrize("Ts", [(1, 8, 40, 64), (65, 100, 168, 192)])
