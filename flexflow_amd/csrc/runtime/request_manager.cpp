@@ -658,15 +658,19 @@ TreeVerifyBatchConfig RequestManager::prepare_next_batch_verify(
       R.first_token_depth_in_request = (int)request.tokens.size() - 1;
       bool cutLayer = false;
       for (size_t j = 1; j < tree.size(); j++) {
+        // the batch is full with tree tokens left: drop the partially
+        // included last layer (:2055-2091).  Checked before placing token j:
+        // the root itself can take the last slot of `limit`, and then there
+        // is no tree layer to drop (the request verifies its root alone)
+        if (new_bc.num_tokens == limit) {
+          cutLayer = j > 1;
+          break;
+        }
         new_bc.tokensInfo[new_bc.num_tokens].request_index = i;
         new_bc.tokensInfo[new_bc.num_tokens].token_id = tree[j].first;
         new_bc.tokensInfo[new_bc.num_tokens].abs_depth_in_request = tree[j].second;
         new_bc.num_tokens++;
         R.num_tokens_in_batch++;
-        if (new_bc.num_tokens == limit && j != tree.size() - 1) {
-          cutLayer = true;
-          break;
-        }
       }
       if (cutLayer) {  // drop the partially included last layer
         const int total_tokens = new_bc.num_tokens;

@@ -50,25 +50,25 @@ def prompts(n, V, lo=3, hi=40, seed=0):
 V = 997
 
 
-def run_incr(ps, max_length, batch=4, max_tokens=16, eos=()):
+def run_incr(ps, max_length, batch=4, max_tokens=16, eos=(), msl=128):
     rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
-                           max_sequence_length=128, eos_token_ids=eos)
-    llm = fa.HashModel(V, "inc", max_requests=batch, max_seq_len=128)
+                           max_sequence_length=msl, eos_token_ids=eos)
+    llm = fa.HashModel(V, "inc", max_requests=batch, max_seq_len=msl)
     res = fa.generate(rm, llm, ps, max_length=max_length)
     return res, rm.stats()
 
 
 def run_spec(ps, max_length, batch=4, max_tokens=64, widths=(1, 1, 3), disagree=0,
-             tree_tokens=23, ssms=None, ext=0, eos=()):
+             tree_tokens=23, ssms=None, ext=0, eos=(), msl=128):
     """ssms: [(salt, disagree_pct)] per SSM (default one SSM, salt 1234)."""
     rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=max_tokens,
-                           max_sequence_length=128, spec_tree_width=widths,
+                           max_sequence_length=msl, spec_tree_width=widths,
                            max_spec_tree_token_num=tree_tokens, spec_extensions=ext,
                            eos_token_ids=eos)
-    llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=128,
+    llm = fa.HashModel(V, "tree", max_requests=batch, max_seq_len=msl,
                        max_tree_tokens=tree_tokens)
     for salt, dis in ssms or [(1234, disagree)]:
-        rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=batch, max_seq_len=128,
+        rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=batch, max_seq_len=msl,
                                            max_tree_tokens=tree_tokens, salt=salt,
                                            disagree_pct=dis))
     res = fa.generate(rm, llm, ps, max_length=max_length)
@@ -336,3 +336,37 @@ def test_incr_decoding_randomized_configs(seed):
                       eos=eos)
     for p, q in zip(ps, res):
         assert q.output_tokens == expected(p, ml, V, eos=eos), seed
+
+
+@pytest.mark.parametrize("block", range(4))
+def test_spec_infer_randomized_sequence_limits(block):
+    """Random max_sequence_length (48-512) with max_length up to its last
+    allowed value (the reference rejects max_length >= max_sequence_length,
+    request_manager.cc:386-391), long prompts loaded in chunks, random trees
+    and SSMs: SpecInfer == incremental decoding == greedy, so commits and
+    tree slots near the end of each request's cache rows stay exact."""
+    import random
+    checked = 0
+    for seed in range(OFF + 50000 + block * 25, OFF + 50000 + block * 25 + 25):
+        r = random.Random(seed)
+        msl = r.choice([48, 64, 100, 128, 256, 512])
+        batch = r.choice([1, 2, 4, 8])
+        mt = r.choice([16, 32, 64, 128])
+        widths = r.choice(WIDTHS)
+        nssm = r.choice([1, 1, 2, 4])
+        tree = r.choice([16, 23, 27, 48, 64])
+        ssms = [(r.randrange(1, 10000), r.choice([0, 10, 50, 100])) for _ in range(nssm)]
+        ps = prompts(r.randint(1, 8), V, lo=1, hi=max(2, msl // 2), seed=seed)
+        ml = r.randint(max(len(p) for p in ps) + 2, msl - 1)
+        try:
+            res, _ = run_spec(ps, ml, batch=batch, max_tokens=mt, widths=widths, tree_tokens=tree,
+                              ssms=ssms, ext=W4 | (MULTI if nssm > 1 else 0), msl=msl)
+        except fa.ffmi.FFMIError as e:
+            assert "SSM loaded less" in str(e), (seed, str(e))
+            continue
+        inc, _ = run_incr(ps, ml, batch=batch, max_tokens=mt, msl=msl)
+        for p, q, i in zip(ps, res, inc):
+            want = expected(p, ml, V)
+            assert q.output_tokens == want and i.output_tokens == want, (seed, msl, ml)
+        checked += 1
+    assert checked >= 15
