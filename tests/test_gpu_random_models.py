@@ -3,7 +3,8 @@
 random FFN width and vocabulary,
 RoPE theta, RMS eps), random scheduler limits (batch slots, token budget) and
 random request mixes (1-10 prompts of 1-60 tokens, queued past the slots),
-through the MI355X path:
+random max_sequence_length (64, 128 or 256; max_length up to its last
+allowed value), through the MI355X path:
 
   * incremental decoding: every request's tokens teacher-forced through the
     oracle under the tie rule of tests/parity_rules.py (a mismatch must be a
@@ -76,10 +77,12 @@ def random_cfg(rng, vocab=None, inc=False):
                 rope_theta=float(rng.choice([10000.0, 500000.0])))
 
 
-def random_requests(rng, V):
+def random_requests(rng, V, msl=128):
+    """1-10 prompts of up to min(60, msl / 2) tokens and a max_length below
+    max_sequence_length (the reference rejects max_length >= it)"""
     n = int(rng.integers(1, 11))
-    ps = [rng.integers(3, V, size=int(rng.integers(1, 61))).tolist() for _ in range(n)]
-    max_length = min(127, max(len(p) for p in ps) + 1 + int(rng.integers(8, 40)))
+    ps = [rng.integers(3, V, size=int(rng.integers(1, min(61, msl // 2)))).tolist() for _ in range(n)]
+    max_length = min(msl - 1, max(len(p) for p in ps) + 1 + int(rng.integers(8, 40)))
     return ps, max_length
 
 
@@ -87,12 +90,13 @@ def random_requests(rng, V):
 def test_random_model_incr_decoding_vs_oracle(seed):
     rng = np.random.default_rng(9000 + OFF + seed)
     cfg = random_cfg(rng, inc=True)
-    ps, ml = random_requests(rng, cfg["vocab_size"])
+    msl = int(rng.choice([64, 128, 256]))
+    ps, ml = random_requests(rng, cfg["vocab_size"], msl)
     B = int(rng.choice([1, 2, 3, 4, 8]))
     mtb = int(rng.choice([8, 16, 32, 64, 128]))
     rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
-                           max_sequence_length=128)
-    m = fa.Model(cfg, "inc", max_requests=B, max_tokens=mtb, max_seq_len=128,
+                           max_sequence_length=msl)
+    m = fa.Model(cfg, "inc", max_requests=B, max_tokens=mtb, max_seq_len=msl,
                  weight_seed=100 + seed)
     try:
         res = fa.generate(rm, m, ps, max_length=ml)
@@ -106,7 +110,8 @@ def test_random_model_spec_infer_vs_oracle(seed):
     rng = np.random.default_rng(9500 + OFF + seed)
     cfg = random_cfg(rng)
     V = cfg["vocab_size"]
-    ps, ml = random_requests(rng, V)
+    msl = int(rng.choice([64, 128, 256]))
+    ps, ml = random_requests(rng, V, msl)
     B = int(rng.choice([1, 2, 4, 8]))
     mtb = int(rng.choice([32, 64, 128]))
     widths = WIDTHS[int(rng.integers(0, len(WIDTHS)))]
@@ -115,9 +120,9 @@ def test_random_model_spec_infer_vs_oracle(seed):
     ext = fa.ffmi.SPEC_EXT_WIDTH4 | (fa.ffmi.SPEC_EXT_MULTI_SSM if nssm > 1 else 0)
     vt = mtb + tree * B
     rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
-                           max_sequence_length=128, spec_tree_width=widths,
+                           max_sequence_length=msl, spec_tree_width=widths,
                            max_spec_tree_token_num=tree, spec_extensions=ext)
-    llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
+    llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=msl,
                    max_tree_tokens=tree, weight_seed=200 + seed)
     # SSMs: random smaller models over the same vocabulary, or (agreeing
     # fully) the LLM's own shape and weights, for long accepted paths
@@ -125,7 +130,7 @@ def test_random_model_spec_infer_vs_oracle(seed):
     for k in range(nssm):
         same = rng.random() < 0.3
         scfg = cfg if same else random_cfg(rng, vocab=V)
-        ssms.append(fa.Model(scfg, "beam", max_requests=B, max_tokens=vt, max_seq_len=128,
+        ssms.append(fa.Model(scfg, "beam", max_requests=B, max_tokens=vt, max_seq_len=msl,
                              max_tree_tokens=tree, weight_seed=200 + seed if same else 300 + k))
         rm.register_ssm_model(ssms[-1])
     try:
