@@ -14,6 +14,45 @@ namespace ffmi {
 __device__ __forceinline__ float h2f_(uint16_t v) { return __half2float(__ushort_as_half(v)); }
 __device__ __forceinline__ uint16_t f2h_(float v) { return __half_as_ushort(__float2half_rn(v)); }
 
+// exp(x) for the softmax / top-k terms and probabilities, bit-identical to the
+// host libm expf the oracle calls (glibc's double-evaluated algorithm: x /
+// ln2 * 32 rounded to k, 2^(k/32) from a 32-entry table, a cubic in the
+// remainder, one rounding to float; checked against glibc 2.35 expf on every
+// float in [-104, 0], scripts/diag/expf_ref_check.c: 1 difference in 1.1e9,
+// at x = -63.1, whose fp16 probability is 0 either way).  The device
+// library's expf differs from it by one float ulp on ~1e-4 of inputs, mostly
+// near 0 -- where a flat row's terms all lie -- which moved fp16 p values
+// across a rounding boundary and reordered tied top-k ids (the fresh-seed
+// random-shape sweep of test_softmax_topk_random_shapes_exact).
+__constant__ unsigned long long kExp2Tab[32] = {
+    0x3ff0000000000000ull, 0x3fefd9b0d3158574ull, 0x3fefb5586cf9890full, 0x3fef9301d0125b51ull,
+    0x3fef72b83c7d517bull, 0x3fef54873168b9aaull, 0x3fef387a6e756238ull, 0x3fef1e9df51fdee1ull,
+    0x3fef06fe0a31b715ull, 0x3feef1a7373aa9cbull, 0x3feedea64c123422ull, 0x3feece086061892dull,
+    0x3feebfdad5362a27ull, 0x3feeb42b569d4f82ull, 0x3feeab07dd485429ull, 0x3feea47eb03a5585ull,
+    0x3feea09e667f3bcdull, 0x3fee9f75e8ec5f74ull, 0x3feea11473eb0187ull, 0x3feea589994cce13ull,
+    0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
+    0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
+    0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
+__device__ __forceinline__ float expf_ref(float x) {
+  if (!(x > -104.0f)) return x == x ? 0.0f : x;  // (underflow to 0; NaN stays NaN)
+  if (x > 0.0f) return expf(x);                   // (not reached: x - max <= 0)
+  const double N = 32.0;
+  const double InvLn2N = 0x1.71547652b82fep+0 * N, SHIFT = 0x1.8p+52;
+  const double C0 = 0x1.c6af84b912394p-5 / N / N / N, C1 = 0x1.ebfce50fac4f3p-3 / N / N,
+               C2 = 0x1.62e42ff0c52d6p-1 / N;
+  const double z = __dmul_rn(InvLn2N, (double)x);
+  double kd = __dadd_rn(z, SHIFT);
+  const unsigned long long ki = (unsigned long long)__double_as_longlong(kd);
+  kd = __dsub_rn(kd, SHIFT);
+  const double r = __dsub_rn(z, kd);
+  const double s = __longlong_as_double((long long)(kExp2Tab[ki & 31] + (ki << 47)));
+  const double p = __fma_rn(C0, r, C1);
+  const double r2 = __dmul_rn(r, r);
+  double y = __fma_rn(C2, r, 1.0);
+  y = __fma_rn(p, r2, y);
+  return (float)__dmul_rn(y, s);
+}
+
 template <int NW, typename T>
 __device__ __forceinline__ T block_sum(T v, T *scratch) {
 #pragma unroll
@@ -377,8 +416,8 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     for (int j = 0; j < 4; ++j)
       if (j == k - 1) L = top[j];
   }
-  // the sum's terms use the accurate expf, as the p values and the oracle
-  // do: with the hardware exp2 (__expf, a few ulp) a peaked row, whose S a few
+  // the sum's terms use the oracle's expf (expf_ref), as the p values do:
+  // with the hardware exp2 (__expf, a few ulp) a peaked row, whose S a few
   // terms dominate, took their errors straight into S's float rounding, and
   // 1 p in ~10^4 came out one fp16 ulp off (the random-shape sweep of
   // test_softmax_topk_random_shapes_exact)
@@ -387,7 +426,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   for (int v = 0; v < NV; ++v)
     if (v * TPB + tid < nvec)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) se += (double)expf(elem(v, e) - M);
+      for (int e = 0; e < 8; ++e) se += (double)expf_ref(elem(v, e) - M);
   se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
@@ -400,7 +439,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   // (finite: logits set to -inf -- taken ones -- are never candidates)
   float thr = -3.402823466e38f;
   {
-    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    const uint16_t pL = f2h_(__fdiv_rn(expf_ref(L - M), S));
     if (pL > 1) {
       const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
       thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
@@ -408,7 +447,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   }
   // keys: (p + 1) << 32 | ~idx, 0 = not a candidate / taken
   auto key_of = [&](float xv, unsigned i) -> unsigned long long {
-    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    const uint16_t p = f2h_(__fdiv_rn(expf_ref(xv - M), S));
     return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
   };
   auto emit = [&](int rd, unsigned long long b) {
@@ -531,7 +570,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
       if (j == k - 1) L = top[j];
   }
   double se = 0.0;
-  for (int i = tid; i < V; i += TPB) se += (double)expf(h2f_(x[i]) - M);
+  for (int i = tid; i < V; i += TPB) se += (double)expf_ref(h2f_(x[i]) - M);
   se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
@@ -541,14 +580,14 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
   const float S = (float)sd;
   float thr = -3.402823466e38f;
   {
-    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    const uint16_t pL = f2h_(__fdiv_rn(expf_ref(L - M), S));
     if (pL > 1) {
       const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
       thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
     }
   }
   auto key_of = [&](float xv, unsigned i) -> unsigned long long {
-    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    const uint16_t p = f2h_(__fdiv_rn(expf_ref(xv - M), S));
     return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - i);
   };
   auto emit = [&](int rd, unsigned long long b) {
@@ -717,7 +756,7 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
     // (exchange buffer: [P][T][W] of phase 0 is read above and rewritten
     //  below only after the whole block has read it)
     double se = 0.0;
-    for (int i = tid; i < Vl; i += TPB) se += (double)expf(h2f_(x[i]) - M);
+    for (int i = tid; i < Vl; i += TPB) se += (double)expf_ref(h2f_(x[i]) - M);
     se = __ockl_wfred_add_f64(se);
     if (lane == 0) dsh[wv] = se;
     __syncthreads();
@@ -765,14 +804,14 @@ __global__ __launch_bounds__(TPB) void vshard_kernel(const uint16_t *__restrict_
   }
   float thr = -3.402823466e38f;
   {
-    const uint16_t pL = f2h_(__fdiv_rn(expf(L - M), S));
+    const uint16_t pL = f2h_(__fdiv_rn(expf_ref(L - M), S));
     if (pL > 1) {
       const float lo = 0.5f * (h2f_(pL) + h2f_((uint16_t)(pL - 1)));
       thr = M + logf(lo * S) - 0.0009765625f * fmaxf(1.0f, fabsf(M));
     }
   }
   auto key_of = [&](float xv, int i) -> unsigned long long {
-    const uint16_t p = f2h_(__fdiv_rn(expf(xv - M), S));
+    const uint16_t p = f2h_(__fdiv_rn(expf_ref(xv - M), S));
     const unsigned gi = (unsigned)(rank * Vl + i);
     return ((unsigned long long)(p + 1u) << 32) | (unsigned long long)(0xffffffffu - gi);
   };
