@@ -592,6 +592,17 @@ extern "C" ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, in
   return FFMI_OK;
 }
 
+extern "C" size_t ffmi_arg_topk_workspace_bytes(int T) { return ffmi::argmax_workspace_bytes(T); }
+
+extern "C" ffmi_status ffmi_arg_topk_ws(const void *logits, int T, int V, int k, int32_t *ids,
+                                        float *probs, void *workspace, size_t workspace_bytes,
+                                        ffmi_stream stream) {
+  FFMI_CHECK(logits && ids && V > 0 && k >= 1 && k <= 4 && k <= V, FFMI_ERR_INVALID);
+  FFMI_HIP(ffmi::launch_argmax((const uint16_t *)logits, T, V, k, ids, probs,
+                               (hipStream_t)stream, workspace, workspace_bytes));
+  return FFMI_OK;
+}
+
 // Test hooks of the residual RMSNorm folded into the decode GEMMs (the pair
 // llama_gpu.cpp runs at T <= 32): the producer adds its rounded output to
 // the residual in place and leaves per-(row, 16-column tile) sums of

@@ -204,15 +204,20 @@ hipError_t launch_pack_act(const uint16_t *X, uint16_t *Xp, int T, int K, hipStr
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
                           hipStream_t s, bool out_packed = false, Partials x2p = {}, const char *gather = nullptr,
-                          char *blob_dst = nullptr, size_t blob_bytes = 0);
+                          char *blob_dst = nullptr, size_t blob_bytes = 0,
+                          const int32_t *gather_prev = nullptr);
 // FFMI_FAULT_RESID_ROUND negative control (tests only; process-wide)
 void set_norm_fault(bool on);
 hipError_t launch_embedding(const char *blob, int T, const uint16_t *table,
                             uint16_t *out, int H, hipStream_t s);
 hipError_t launch_silu_mul(const uint16_t *a, const uint16_t *b, uint16_t *out,
                            size_t n, hipStream_t s);
+// softmax + argmax / top-k; with a zeroed workspace of argmax_workspace_bytes(T)
+// (left zeroed) rows of a small T are split over several workgroups
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
-                         float *probs, hipStream_t s);
+                         float *probs, hipStream_t s, void *ws = nullptr, size_t ws_bytes = 0,
+                         int32_t *ids2 = nullptr);  // (ids2: a second copy of the ids)
+size_t argmax_workspace_bytes(int T);
 // Vocab-sharded tail (norm.hip): phase 0..2 write this rank's exchange
 // record ([P][T][W] floats, W >= max(4, 2k)); phase 3 merges into ids/probs.
 hipError_t launch_vshard(const uint16_t *logits, int T, int Vl, int P, int rank, int k,

@@ -33,9 +33,7 @@ __constant__ unsigned long long kExp2Tab[32] = {
     0x3feeace5422aa0dbull, 0x3feeb737b0cdc5e5ull, 0x3feec49182a3f090ull, 0x3feed503b23e255dull,
     0x3feee89f995ad3adull, 0x3feeff76f2fb5e47ull, 0x3fef199bdd85529cull, 0x3fef3720dcef9069ull,
     0x3fef5818dcfba487ull, 0x3fef7c97337b9b5full, 0x3fefa4afa2a490daull, 0x3fefd0765b6e4540ull};
-__device__ __forceinline__ float expf_ref(float x) {
-  if (!(x > -104.0f)) return x == x ? 0.0f : x;  // (underflow to 0; NaN stays NaN)
-  if (x > 0.0f) return expf(x);                   // (not reached: x - max <= 0)
+__device__ __forceinline__ float expf_ref_core(float x) {
   const double N = 32.0;
   const double InvLn2N = 0x1.71547652b82fep+0 * N, SHIFT = 0x1.8p+52;
   const double C0 = 0x1.c6af84b912394p-5 / N / N / N, C1 = 0x1.ebfce50fac4f3p-3 / N / N,
@@ -51,6 +49,16 @@ __device__ __forceinline__ float expf_ref(float x) {
   double y = __fma_rn(C2, r, 1.0);
   y = __fma_rn(p, r2, y);
   return (float)__dmul_rn(y, s);
+}
+// Branch-free (every caller passes x = logit - row max <= 0): the formula runs
+// on max(x, -104) and the result is selected, so an unrolled loop of terms
+// issues all its table loads ahead of the arithmetic instead of one
+// load-and-wait per term behind per-element branches.
+__device__ __forceinline__ float expf_ref(float x) {
+  const bool in = x > -104.0f;
+  const float xr = in ? x : -104.0f;  // (NaN and -inf too: selected away below)
+  const float y = expf_ref_core(xr);
+  return in ? y : (x == x ? 0.0f : x);  // (underflow to 0; NaN stays NaN)
 }
 
 template <int NW, typename T>
@@ -86,7 +94,7 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
     const uint16_t *__restrict__ w, uint16_t *__restrict__ res_out,
     uint16_t *__restrict__ out, int H, float eps, int out_packed,
     const float *__restrict__ x2p, int pS, int pNP, const char *__restrict__ gather,
-    uint4 *__restrict__ blob_dst, int blob_n16) {
+    uint4 *__restrict__ blob_dst, int blob_n16, const int32_t *__restrict__ gprev) {
   __shared__ double scratch[NT / 64];
   const int row = blockIdx.x;
   const int T = gridDim.x;
@@ -95,8 +103,15 @@ __global__ __launch_bounds__(NT) void rmsnorm_kernel(
   // embedding lookup fused into the first layer's norm; res_out gets the copy)
   constexpr bool FAULT = SRC >= 4;
   constexpr int S = FAULT ? SRC - 3 : SRC;  // the data source of the variant
-  const uint16_t *a = S == 3 ? x1 + (size_t)batch_view(gather).tokens[row].token_id * H
-                             : x1 + (size_t)row * H;
+  // (a chained SSM beam step: token id -1 - i is entry i of the previous
+  // step's top-k ids, gprev, which the host could not know when it staged
+  // this step; ffmi_model beam_launch_chained)
+  int gid = 0;
+  if (S == 3) {
+    gid = batch_view(gather).tokens[row].token_id;
+    if (gid < 0) gid = gprev[-1 - gid];
+  }
+  const uint16_t *a = S == 3 ? x1 + (size_t)gid * H : x1 + (size_t)row * H;
   // blob fetch: gather is the step's staging blob in mapped host memory; the
   // grid copies it into device memory for the step's later kernels (replaces
   // the H2D copy node and the system-scope boundary after it), its loads in
@@ -215,7 +230,7 @@ void set_norm_fault(bool on) { g_norm_fault = on; }
 hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t *w,
                           uint16_t *res_out, uint16_t *out, int T, int H, float eps,
                           hipStream_t s, bool out_packed, Partials x2p, const char *gather,
-                          char *blob_dst, size_t blob_bytes) {
+                          char *blob_dst, size_t blob_bytes, const int32_t *gather_prev) {
   if (gather && (x2 || x2p.S > 0 || !res_out)) return hipErrorInvalidValue;
   if (blob_dst && (!gather || blob_bytes > (size_t)1 << 30 || (uintptr_t)gather % 16 ||
                    (uintptr_t)blob_dst % 16))
@@ -242,7 +257,7 @@ hipError_t launch_rmsnorm(const uint16_t *x1, const uint16_t *x2, const uint16_t
 #define FFMI_RMS3(NT, MC, MS, SR)                                                              \
   hipLaunchKernelGGL((rmsnorm_kernel<NT, MC, MS, SR>), dim3(T), dim3(NT), 0, s, x1, x2, w,    \
                      res_out, out, H, eps, op, pp, x2p.S, x2p.NP, gather,               \
-                     reinterpret_cast<uint4 *>(blob_dst), blob_n16)
+                     reinterpret_cast<uint4 *>(blob_dst), blob_n16, gather_prev)
 #define FFMI_RMS(NT, MC)                                   \
   do {                                                     \
     if (src == 0) FFMI_RMS3(NT, MC, 1, 0);                 \
@@ -357,25 +372,52 @@ extern "C" __device__ unsigned long long __ockl_wfred_max_u64(unsigned long long
 //    the k best (k wave reductions, no workgroup barrier).  More than kCand
 //    candidates (flat rows, planted ties) fall back to k rounds of a
 //    workgroup-wide selection over the registers.
-template <int TPB, int NV>
+//  * G > 1 (few rows: the SSM's beam steps, decode): G workgroups per row
+//    (grid G x T), each loading the whole row (max and wave maxima identical
+//    in all of them) but summing the exp terms of only 1/G of every thread's
+//    elements: the double-precision expf_ref terms are the kernel's cost, and
+//    T = 24 rows kept them on 24 CUs.  Each workgroup publishes its partial
+//    sum (one lane: agent-scope store, drained, then an agent-scope add on
+//    the row's counter); the workgroup whose add comes last reads the G
+//    partials by atomic reads, sums them in chunk order, resets the counter
+//    and finishes the row from its registers.  No workgroup waits for
+//    another.  The double sum is split differently than at G = 1 (and than
+//    the oracle's serial loop): S = float(double sum) in any order, as above.
+//    `part` = [T][G] doubles, `cnt` = [T] counters, zero before the first
+//    launch and left zero.
+template <int TPB, int NV, int G>
 __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
-    float *__restrict__ probs) {
+    float *__restrict__ probs, double *__restrict__ part, unsigned *__restrict__ cnt,
+    int32_t *__restrict__ ids2) {
   constexpr int NW = TPB / 64;
   constexpr int kCand = 128;
+  static_assert(G == 1 || ((NV * 8) % G == 0 && NV * 8 / G >= 2),
+                "split: whole dwords of a thread's elements per workgroup");
+  constexpr int E = NV * 8 / G;  // elements of each thread's row part this workgroup sums
   // wave maxima / sums / selection keys, and the candidate list
   __shared__ double sh[NW + 2];
   __shared__ unsigned long long cand[kCand];
   __shared__ unsigned ncand;
+  __shared__ int last_arrival;
   float *fsh = reinterpret_cast<float *>(sh);
   unsigned long long *ksh = reinterpret_cast<unsigned long long *>(sh);
-  const int row = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int row = G == 1 ? blockIdx.x : blockIdx.y, chunk = G == 1 ? 0 : blockIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nvec = V >> 3;
   const uint4 *x = reinterpret_cast<const uint4 *>(logits + (size_t)row * V);
+  // split form: workgroup `chunk` loads the row's vectors rotated so that the
+  // elements it sums are always its first E (compile-time register indices):
+  // local vector v holds row vector gv(v); E < 8: a runtime half / quarter of
+  // local vector 0, at element eo
+  constexpr int EPV = E < 8 ? 8 / E : 1;  // workgroups sharing one vector
+  const int vrot = G == 1 ? 0 : (E >= 8 ? chunk * (E / 8) : chunk / EPV);
+  const int eo = E >= 8 ? 0 : (chunk % EPV) * E;
+  auto gv = [&](int v) -> int { return (G == 1 ? v : (v + vrot) % NV) * TPB + tid; };
   uint4 r[NV];
 #pragma unroll
   for (int v = 0; v < NV; ++v) {
-    const int i = v * TPB + tid;
+    const int i = gv(v);
     r[v] = i < nvec ? x[i] : make_uint4(0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u, 0xfc00fc00u);
   }
   if (tid == 0) ncand = 0;
@@ -422,17 +464,65 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   // 1 p in ~10^4 came out one fp16 ulp off (the random-shape sweep of
   // test_softmax_topk_random_shapes_exact)
   double se = 0.0;
+  if constexpr (E >= 8) {
 #pragma unroll
-  for (int v = 0; v < NV; ++v)
-    if (v * TPB + tid < nvec)
+    for (int v = 0; v < E / 8; ++v)
+      if (gv(v) < nvec)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) se += (double)expf_ref(elem(v, e) - M);
+        for (int e = 0; e < 8; ++e) se += (double)expf_ref(elem(v, e) - M);
+  } else {
+    // dwords eo/2 .. eo/2 + E/2 - 1 of local vector 0 (selects, no indexing)
+    const int d0 = eo >> 1;
+    auto dw = [&](int d) -> uint32_t {  // selects (a runtime array index would go to scratch)
+      const uint32_t lo = (d & 1) ? r[0].y : r[0].x, hi = (d & 1) ? r[0].w : r[0].z;
+      return (d & 2) ? hi : lo;
+    };
+    if (gv(0) < nvec)
+#pragma unroll
+      for (int q = 0; q < E / 2; ++q) {
+        const uint32_t w = dw(d0 + q);
+        se += (double)expf_ref(h2f_((uint16_t)(w & 0xffffu)) - M);
+        se += (double)expf_ref(h2f_((uint16_t)(w >> 16)) - M);
+      }
+  }
   se = __ockl_wfred_add_f64(se);
   if (lane == 0) sh[wv] = se;
   __syncthreads();
   double sd = 0.0;
 #pragma unroll
   for (int q = 0; q < NW; ++q) sd += sh[q];
+  if constexpr (G > 1) {
+    // (the guide's single-counter hand-off: agent-scope store of the bytes,
+    // drained, then the add; the last adder reads them with agent-scope
+    // loads after its add returned -- one load per lane, all in flight)
+    if (wv == 0) {
+      unsigned before = 0;
+      if (lane == 0) {
+        __hip_atomic_store(&part[(size_t)row * G + chunk], sd, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        before = __hip_atomic_fetch_add(&cnt[row], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const int last = __shfl(before, 0) == (unsigned)(G - 1);
+      if (last) {
+        double pq = 0.0;
+        if (lane < G)
+          pq = __hip_atomic_load(&part[(size_t)row * G + lane], __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+        double tot = 0.0;
+#pragma unroll
+        for (int q = 0; q < G; ++q) tot += __shfl(pq, q);  // chunk order
+        if (lane == 0) {
+          __hip_atomic_store(&cnt[row], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          sh[NW] = tot;
+        }
+      }
+      if (lane == 0) last_arrival = last;
+    }
+    __syncthreads();
+    if (!last_arrival) return;
+    sd = sh[NW];
+  }
   const float S = (float)sd;
   // candidate threshold from p(L): its lower fp16 rounding boundary, minus a
   // margin of 2^-10 in x (>> the float error of exp, the division and log)
@@ -452,6 +542,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
   };
   auto emit = [&](int rd, unsigned long long b) {
     ids[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    if (ids2) ids2[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
     if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
   };
 #pragma unroll
@@ -459,7 +550,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float xv = elem(v, e);
-      const unsigned i = (unsigned)((v * TPB + tid) * 8 + e);
+      const unsigned i = (unsigned)(gv(v) * 8 + e);
       if (xv >= thr && (int)i < V) {
         const unsigned slot = atomicAdd(&ncand, 1u);
         if (slot < (unsigned)kCand) cand[slot] = key_of(xv, i);
@@ -488,7 +579,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
 #pragma unroll
       for (int e = 0; e < 8; ++e) {
         const float xv = elem(v, e);
-        const unsigned i = (unsigned)((v * TPB + tid) * 8 + e);
+        const unsigned i = (unsigned)(gv(v) * 8 + e);
         if (xv >= thr && (int)i < V) {
           const unsigned long long key = key_of(xv, i);
           best = key > best ? key : best;
@@ -506,11 +597,15 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
     if (rd + 1 < k && (idx >> 3) % TPB == (unsigned)tid) {  // owner marks it taken (-inf)
 #pragma unroll
       for (int v = 0; v < NV; ++v)
-        if ((unsigned)(v * TPB + tid) == (idx >> 3)) {
-          uint16_t *ph = reinterpret_cast<uint16_t *>(&r[v]);
+        if ((unsigned)gv(v) == (idx >> 3)) {
+          // (compile-time register indices only: a runtime-indexed store
+          // into the row's registers would put it in scratch)
 #pragma unroll
-          for (int e = 0; e < 8; ++e)
-            if ((unsigned)e == (idx & 7)) ph[e] = 0xfc00;
+          for (int e = 0; e < 8; ++e) {
+            uint32_t &w = (&r[v].x)[e >> 1];
+            const uint32_t m = (e & 1) ? 0xffff0000u : 0x0000ffffu;
+            if ((unsigned)e == (idx & 7)) w = (w & ~m) | (0xfc00fc00u & m);
+          }
         }
     }
   }
@@ -528,7 +623,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_reg_kernel(
 template <int TPB>
 __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
     const uint16_t *__restrict__ logits, int V, int k, int32_t *__restrict__ ids,
-    float *__restrict__ probs) {
+    float *__restrict__ probs, int32_t *__restrict__ ids2) {
   constexpr int NW = TPB / 64;
   constexpr int kCand = 128;
   __shared__ double sh[NW + 2];
@@ -592,6 +687,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
   };
   auto emit = [&](int rd, unsigned long long b) {
     ids[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
+    if (ids2) ids2[(size_t)row * k + rd] = (int)(0xffffffffu - (unsigned)(b & 0xffffffffu));
     if (probs) probs[(size_t)row * k + rd] = h2f_((uint16_t)((b >> 32) - 1u));
   };
   for (int i = tid; i < V; i += TPB) {
@@ -641,10 +737,27 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
   }
 }
 
+// split-row workspace: [kSplitRows] row counters at a FIXED offset (one
+// workspace serves steps of every T: a counter must never share bytes with
+// another T's partials), then [T][G <= 16] partial sums
+constexpr int kSplitRows = 128;
+constexpr size_t kSplitPartOff = kSplitRows * 4;
+size_t argmax_workspace_bytes(int T) {
+  return T <= 0 ? 0 : kSplitPartOff + (size_t)std::min(T, kSplitRows) * 16 * 8;
+}
+
 hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *ids,
-                         float *probs, hipStream_t s) {
+                         float *probs, hipStream_t s, void *ws, size_t ws_bytes, int32_t *ids2) {
   if (T <= 0) return hipSuccess;
   if (k < 1 || k > 4) return hipErrorInvalidValue;
+  // workgroups per row (the split form needs the caller's zeroed workspace):
+  // T x G <= 256, one workgroup per CU; FFMI_TOPK_SPLIT = 0 (off) / G (forced)
+  static const int split_env = getenv("FFMI_TOPK_SPLIT") ? atoi(getenv("FFMI_TOPK_SPLIT")) : -1;
+  int G = T <= 16 ? 16 : T <= 32 ? 8 : T <= 64 ? 4 : T <= kSplitRows ? 2 : 1;
+  if (split_env >= 0) G = split_env;
+  if (!ws || ws_bytes < argmax_workspace_bytes(T) || T > kSplitRows) G = 1;
+  unsigned *cnt = reinterpret_cast<unsigned *>(ws);
+  double *part = ws ? reinterpret_cast<double *>(static_cast<char *>(ws) + kSplitPartOff) : nullptr;
   // workgroup width (A/B: FFMI_TOPK_TPB = 256 / 512 / 1024)
   static const int tpb = [] {
     const char *e = getenv("FFMI_TOPK_TPB");
@@ -655,9 +768,28 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   // (NV = 8 at 1024 threads would spill: larger vocabularies take the loop kernel)
   if (V % 8 == 0 && ((uintptr_t)logits & 15) == 0 && nv * tpb <= 4096) {
 #define FFMI_SMR(TPB, NV)                                                                  \
-  hipLaunchKernelGGL((softmax_topk_reg_kernel<TPB, NV>), dim3(T), dim3(TPB), 0, s, logits, V, \
-                     k, ids, probs)
-    if (tpb == 256) {
+  hipLaunchKernelGGL((softmax_topk_reg_kernel<TPB, NV, 1>), dim3(T), dim3(TPB), 0, s, logits, V, \
+                     k, ids, probs, nullptr, nullptr, ids2)
+#define FFMI_SMG(NV, GG)                                                                     \
+  hipLaunchKernelGGL((softmax_topk_reg_kernel<1024, NV, GG>), dim3(GG, T), dim3(1024), 0, s, \
+                     logits, V, k, ids, probs, part, cnt, ids2)
+    const int gmax = 4 * std::max(1, nv);  // >= 2 of a thread's 8 NV elements per workgroup
+    while (G > 1 && (G > gmax || (G & (G - 1)))) G >>= 1;
+    if (tpb == 1024 && G > 1) {
+      if (nv <= 1) {
+        if (G >= 4) FFMI_SMG(1, 4);
+        else FFMI_SMG(1, 2);
+      } else if (nv <= 2) {
+        if (G >= 8) FFMI_SMG(2, 8);
+        else if (G == 4) FFMI_SMG(2, 4);
+        else FFMI_SMG(2, 2);
+      } else {
+        if (G >= 16) FFMI_SMG(4, 16);
+        else if (G == 8) FFMI_SMG(4, 8);
+        else if (G == 4) FFMI_SMG(4, 4);
+        else FFMI_SMG(4, 2);
+      }
+    } else if (tpb == 256) {
       if (nv <= 4) FFMI_SMR(256, 4);
       else if (nv <= 8) FFMI_SMR(256, 8);
       else FFMI_SMR(256, 16);
@@ -671,8 +803,10 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
       else FFMI_SMR(1024, 4);
     }
 #undef FFMI_SMR
+#undef FFMI_SMG
   } else {
-    hipLaunchKernelGGL(softmax_topk_kernel<1024>, dim3(T), dim3(1024), 0, s, logits, V, k, ids, probs);
+    hipLaunchKernelGGL(softmax_topk_kernel<1024>, dim3(T), dim3(1024), 0, s, logits, V, k, ids, probs,
+                       ids2);
   }
   return hipGetLastError();
 }

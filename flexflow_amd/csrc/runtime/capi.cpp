@@ -183,5 +183,6 @@ extern "C" ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s) {
   s->llm_us = rm->rm.stats.llm_us;
   s->ssm_us = rm->rm.stats.ssm_us;
   s->wall_us = rm->rm.stats.wall_us;
+  s->ssm_phases_chained = rm->rm.stats.ssm_phases_chained;
   return FFMI_OK;
 }

@@ -11,7 +11,9 @@
 //     in batching, tree build, bitmask, verification or commit lists changes a
 //     context and therefore a token.
 // The SSM flavour ranks f(ctx) first with probability (100-disagree)%.
+#include <algorithm>
 #include <array>
+#include <memory>
 #include <vector>
 
 #include "model.h"
@@ -31,6 +33,40 @@ struct HashModel : public ffmi_model {
   int disagree;
   std::vector<int> cache;  // [max_requests][slots]
   std::vector<int> stage;  // previous batch token ids (TREE commits)
+  int cap = -1;            // tokens per step (-1: unbounded), as a GPU model's max_tokens
+  int token_capacity() const override { return cap; }
+  // chained beam steps (model.h), run eagerly: a step's -1 - i token ids are
+  // filled in from the previous slot's results, as the GPU model's gather does
+  static constexpr int kChain = BeamSearchBatchConfig::MAX_BEAM_DEPTH;
+  std::vector<int> slot_ids[kChain];
+  std::vector<float> slot_probs[kChain];
+  size_t last_results = 0;  // scheduler entries of the last beam step
+  bool can_chain_beam() const override { return mode == FFMI_MODEL_BEAM; }
+  ffmi_status beam_launch_chained(const BeamSearchBatchConfig &bc, int slot) override {
+    if (slot < 0 || slot >= kChain) return FFMI_ERR_INVALID;
+    std::unique_ptr<BeamSearchBatchConfig> b(new BeamSearchBatchConfig(bc));
+    for (int t = 0; t < b->num_tokens; ++t) {
+      int &id = b->tokensInfo[t].token_id;
+      if (id >= 0) continue;
+      if (slot == 0 || -1L - id >= (long)slot_ids[slot - 1].size()) return FFMI_ERR_INVALID;
+      id = slot_ids[slot - 1][-1 - id];
+    }
+    std::unique_ptr<BeamInferenceResult> r(new BeamInferenceResult());
+    const ffmi_status st = run_beam(*b, r.get());
+    if (st != FFMI_OK) return st;
+    const size_t n = last_results;  // (scheduler entries: the layout the placeholders index)
+    slot_ids[slot].assign(r->token_ids, r->token_ids + n);
+    slot_probs[slot].assign(r->probs, r->probs + n);
+    return FFMI_OK;
+  }
+  ffmi_status beam_collect_chained(int slot, BeamInferenceResult *ir) override {
+    if (slot < 0 || slot >= kChain) return FFMI_ERR_INVALID;
+    const size_t n = slot_ids[slot].size();
+    std::copy(slot_ids[slot].begin(), slot_ids[slot].end(), ir->token_ids);
+    std::copy(slot_probs[slot].begin(), slot_probs[slot].end(), ir->probs);
+    for (size_t i = 0; i < n; ++i) ir->parent_id[i] = 0;
+    return FFMI_OK;
+  }
 
   int slot_of(int r, int s) const { return r * slots + s; }
 
@@ -65,6 +101,12 @@ struct HashModel : public ffmi_model {
   int next_token(uint64_t h) const { return (int)((h >> 17) % (uint64_t)vocab); }
 
   ffmi_status run_inc(const BatchConfig &bc, InferenceResult *ir) override {
+    if (cap >= 0 && bc.num_tokens > cap) return FFMI_ERR_INVALID;
+    // (as the GPU model: ids outside the vocabulary are rejected, so a
+    // scheduler read past a step's results cannot pass unnoticed)
+    for (int t = 0; t < bc.num_tokens; ++t)
+      if (bc.tokensInfo[t].token_id < 0 || bc.tokensInfo[t].token_id >= vocab)
+        return FFMI_ERR_INVALID;
     PackedStep ps;
     pack_inc(bc, max_requests, slots, &ps);
     std::vector<uint64_t> hs;
@@ -73,6 +115,12 @@ struct HashModel : public ffmi_model {
     return FFMI_OK;
   }
   ffmi_status run_tree(const TreeVerifyBatchConfig &bc, InferenceResult *ir) override {
+    if (cap >= 0 && bc.num_tokens > cap) return FFMI_ERR_INVALID;
+    // (as the GPU model: ids outside the vocabulary are rejected, so a
+    // scheduler read past a step's results cannot pass unnoticed)
+    for (int t = 0; t < bc.num_tokens; ++t)
+      if (bc.tokensInfo[t].token_id < 0 || bc.tokensInfo[t].token_id >= vocab)
+        return FFMI_ERR_INVALID;
     PackedStep ps;
     pack_tree(bc, max_requests, slots, &ps);
     std::vector<uint64_t> hs;
@@ -81,11 +129,20 @@ struct HashModel : public ffmi_model {
     return FFMI_OK;
   }
   ffmi_status run_beam(const BeamSearchBatchConfig &bc, BeamInferenceResult *ir) override {
+    if (cap >= 0 && bc.num_tokens > cap) return FFMI_ERR_INVALID;
+    // (as the GPU model: ids outside the vocabulary are rejected, so a
+    // scheduler read past a step's results cannot pass unnoticed)
+    for (int t = 0; t < bc.num_tokens; ++t)
+      if (bc.tokensInfo[t].token_id < 0 || bc.tokensInfo[t].token_id >= vocab)
+        return FFMI_ERR_INVALID;
     PackedStep ps;
     pack_beam(bc, max_requests, slots, &ps);
     std::vector<uint64_t> hs;
     contexts(ps, &hs);
     const int k = ps.topk;
+    // [T][k] as the GPU model's top-k writes it, then the scheduler's layout
+    std::vector<int> ids(hs.size() * k);
+    std::vector<float> prs(hs.size() * k);
     for (size_t t = 0; t < hs.size(); ++t) {
       const uint64_t h = hs[t];
       const int c0 = next_token(h);
@@ -96,11 +153,20 @@ struct HashModel : public ffmi_model {
       std::array<int, 4> rank = agree ? std::array<int, 4>{c0, c1, c2, c3}
                                       : std::array<int, 4>{c1, c0, c2, c3};
       for (int j = 0; j < k; ++j) {
-        ir->token_ids[t * k + j] = rank[j % 4];
-        ir->probs[t * k + j] = 1.0f / (float)(1 << j);
-        ir->parent_id[t * k + j] = 0;
+        ids[t * k + j] = rank[j % 4];
+        prs[t * k + j] = 1.0f / (float)(1 << j);
       }
     }
+    std::vector<int> map;
+    beam_result_layout(bc, &map);
+    for (size_t i = 0; i < map.size(); ++i) {
+      ir->token_ids[i] = ids[map[i]];
+      ir->probs[i] = prs[map[i]];
+      ir->parent_id[i] = 0;
+    }
+    // entries past the step's results: out of the vocabulary (see above)
+    for (size_t i = map.size(); i < map.size() + 4 * hs.size() + 4; ++i) ir->token_ids[i] = -7777;
+    last_results = map.size();
     return FFMI_OK;
   }
 };
@@ -130,4 +196,11 @@ extern "C" ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_
   if (!out) return FFMI_ERR_INVALID;
   return ffmi::create_hash_model(vocab, mode, max_requests, max_seq, max_tree, salt,
                                  disagree_pct, out);
+}
+
+extern "C" ffmi_status ffmi_test_hash_model_set_capacity(ffmi_model *m, int max_tokens) {
+  ffmi::HashModel *h = dynamic_cast<ffmi::HashModel *>(m);
+  if (!h) return FFMI_ERR_INVALID;
+  h->cap = max_tokens;
+  return FFMI_OK;
 }

@@ -36,6 +36,8 @@ struct LayerF {
 struct LlamaF32 : public ffmi_model {
   ffmi_llama_config c{};
   ffmi_model_opts o{};
+  int token_capacity() const override { return o.max_tokens; }
+  bool uses_collectives() const override { return o.tp_size > 1; }
   std::string weights_folder;
   int H = 0, F = 0, V = 0, d = 0, heads_l = 0, Hl = 0, Fl = 0, P = 1, slots = 0, Tm = 0;
   hipStream_t stream = nullptr;
@@ -413,9 +415,14 @@ struct LlamaF32 : public ffmi_model {
     ffmi_status st = forward(k);
     if (st != FFMI_OK) return st;
     const size_t n = (size_t)bc.num_tokens * k;
-    memcpy(ir->token_ids, res_h, n * sizeof(int32_t));
-    memcpy(ir->probs, reinterpret_cast<float *>(res_h + n), n * sizeof(float));
-    for (size_t i = 0; i < n; ++i) ir->parent_id[i] = 0;
+    const float *pr = reinterpret_cast<const float *>(res_h + n);
+    std::vector<int> map;
+    beam_result_layout(bc, &map);
+    for (size_t i = 0; i < map.size(); ++i) {
+      ir->token_ids[i] = res_h[map[i]];
+      ir->probs[i] = pr[map[i]];
+      ir->parent_id[i] = 0;
+    }
     return FFMI_OK;
   }
 };

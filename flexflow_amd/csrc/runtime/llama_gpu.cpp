@@ -24,6 +24,7 @@
 #include <vector>
 
 #include "model.h"
+#include "request_manager.h"  // (now_us)
 
 namespace ffmi {
 
@@ -38,6 +39,8 @@ struct Layer {
 struct LlamaGPU : public ffmi_model {
   ffmi_llama_config c{};
   ffmi_model_opts o{};
+  int token_capacity() const override { return o.max_tokens; }
+  bool uses_collectives() const override { return o.tp_size > 1; }
   std::string weights_folder;  // reference-format checkpoint ("" = synthetic)
   int Hl = 0, Fl = 0, d = 0, heads_l = 0, slots = 0;
   // GEMM inputs (normed hidden, attention output, SiLU output) are kept in
@@ -55,6 +58,9 @@ struct LlamaGPU : public ffmi_model {
   uint16_t *res = nullptr, *h = nullptr, *qkv = nullptr, *att = nullptr, *proj = nullptr,
            *mlp = nullptr, *logits = nullptr;
   int32_t *ids_d = nullptr;
+  // softmax top-k workspace (the split-row form for small steps; zeroed once)
+  void *topk_ws = nullptr;
+  size_t topk_ws_bytes = 0;
   // vocab-sharded lm_head at TP > 1 (model.cc:3392-3419): this rank's Vl rows
   // and the [P][Tm][kXW] exchange records of the sharded softmax / top-k
   int Vl = 0;
@@ -98,7 +104,20 @@ struct LlamaGPU : public ffmi_model {
   // split-K slabs summed by the all-reduce's copy-in (FFMI_AR_SLABS=0: the
   // GEMM's own reduce pass, A/B runs)
   bool ar_slabs = !getenv("FFMI_AR_SLABS") || atoi(getenv("FFMI_AR_SLABS")) != 0;
-  int32_t *ids_h = nullptr;
+  int32_t *ids_h = nullptr;  // [kChain slots][Tm * 4 ids | Tm * 4 probs], pinned
+  // chained beam steps (beam_launch_chained): one staging blob and one result
+  // slot per step of a speculation phase; the top-k also leaves each slot's
+  // ids in device memory (ids_dev) for the next step's embedding gather
+  static constexpr int kChain = BeamSearchBatchConfig::MAX_BEAM_DEPTH;
+  ffmi_batch_dev *chain_batch[kChain] = {};
+  int32_t *ids_dev = nullptr;  // [kChain][Tm * 4]
+  int cur_slot = 0;
+  size_t slot_results[kChain] = {};  // [T][k] ids of each slot
+  std::vector<int> slot_map[kChain];  // scheduler entry -> [T][k] index (beam_result_layout)
+  hipEvent_t slot_ev[kChain] = {};     // recorded behind each launched slot
+  int last_slot = -1;                  // highest slot launched since the last wait
+  bool chain_ok = !getenv("FFMI_SSM_CHAIN") || atoi(getenv("FFMI_SSM_CHAIN")) != 0;
+  size_t slot_ints() const { return (size_t)((o.max_tokens + 15) & ~15) * 4 * 2; }
   bool result_copy = getenv("FFMI_RESULT_COPY") && atoi(getenv("FFMI_RESULT_COPY")) != 0;
   float *probs_h = nullptr;
   ffmi_batch_dev *batch = nullptr;
@@ -322,6 +341,14 @@ struct LlamaGPU : public ffmi_model {
 
   ~LlamaGPU() override {
     if (stream) (void)hipStreamSynchronize(stream);
+    for (auto &kv : st_sum)
+      fprintf(stderr, "[ffmi step timing] H=%d T=%d steps=%ld launch=%.1f gpu=%.1f wait=%.1f total=%.1f us\n",
+              c.hidden, kv.first, kv.second.n, kv.second.launch / kv.second.n, kv.second.gpu / kv.second.n,
+              kv.second.wait / kv.second.n, kv.second.total / kv.second.n);
+    for (auto e : st_ev)
+      if (e) (void)hipEventDestroy(e);
+    for (auto e : slot_ev)
+      if (e) (void)hipEventDestroy(e);
     clear_graphs();
     for (auto &L : layers) ffmi_attn_destroy(L.attn);
     for (auto e : ev_pool) (void)hipEventDestroy(e);
@@ -330,6 +357,7 @@ struct LlamaGPU : public ffmi_model {
     if (comm_stream) (void)hipStreamDestroy(comm_stream);
     for (void *p : allocs) (void)hipFree(p);
     if (ids_h) (void)hipHostFree(ids_h);
+    for (int i = 1; i < kChain; ++i) ffmi_batch_destroy(chain_batch[i]);
     ffmi_batch_destroy(batch);
     if (stream) (void)hipStreamDestroy(stream);
   }
@@ -443,6 +471,9 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&logits, (size_t)Tm * Vl));
     if (Vl != V) TRY(alloc(&xch, (ffmi_vocab_shard_scratch_bytes(P, Tm) + 3) / 4));
     TRY(alloc(&ids_d, (size_t)Tm * 4 * 2));  // [ids | probs] of a step, one D2H copy
+    topk_ws_bytes = ffmi::argmax_workspace_bytes(std::min(Tm, 128));
+    TRY(alloc((char **)&topk_ws, topk_ws_bytes));
+    FFMI_HIP(hipMemsetAsync(topk_ws, 0, topk_ws_bytes, stream));
     peer = P > 1 && ffmi::comm_has_peer(o.comm, (size_t)Tm * H * 2);
     // an attached transport too small for this model's largest [Tm][H]
     // all-reduce needs RCCL (or the local group) for those steps: refuse at
@@ -494,8 +525,10 @@ struct LlamaGPU : public ffmi_model {
     // coherent (uncached) pinned memory: the sampling kernel's stores go
     // straight over PCIe and are visible to the host once the stream has
     // synchronised, whatever HIP_HOST_COHERENT says
-    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)Tm * 4 * 2 * sizeof(int32_t),
+    FFMI_HIP(hipHostMalloc((void **)&ids_h, (size_t)kChain * Tm * 4 * 2 * sizeof(int32_t),
                            hipHostMallocCoherent | hipHostMallocMapped));
+    if (mode == FFMI_MODEL_BEAM) TRY(alloc(&ids_dev, (size_t)kChain * Tm * 4));
+    chain_batch[0] = batch;
     // weights (seeded synthetic, orc_gen_weight spec), packed for MFMA
     uint16_t *tmp = nullptr;
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
@@ -664,11 +697,11 @@ struct LlamaGPU : public ffmi_model {
   // each -- so their whole step (metadata copy, kernels, result copies) is
   // captured once per batch shape into a HIP graph and replayed.
   struct GraphKey {
-    int T, W, C, k, parity, overlap, fused, max_q;
+    int T, W, C, k, parity, overlap, fused, max_q, slot;
     size_t bytes;
     bool operator<(const GraphKey &o) const {
-      return std::tie(T, W, C, k, parity, overlap, fused, max_q, bytes) <
-             std::tie(o.T, o.W, o.C, o.k, o.parity, o.overlap, o.fused, o.max_q, o.bytes);
+      return std::tie(T, W, C, k, parity, overlap, fused, max_q, slot, bytes) <
+             std::tie(o.T, o.W, o.C, o.k, o.parity, o.overlap, o.fused, o.max_q, o.slot, o.bytes);
     }
   };
   // TREE steps write alternate halves of the attention staging (commits of
@@ -685,6 +718,15 @@ struct LlamaGPU : public ffmi_model {
   // (wait for it); SSM beam steps of several SSMs launch all, then finish
   // each (serve_spec_infer), so their latency-bound steps overlap
   bool inflight = false;
+  // FFMI_STEP_TIMING=1 (diagnostics): per step, host time spent staging and
+  // launching, the GPU span between events around the launch, and the
+  // host's wait; summed per step size and printed at destruction
+  bool step_timing = getenv("FFMI_STEP_TIMING") && atoi(getenv("FFMI_STEP_TIMING")) != 0;
+  hipEvent_t st_ev[2] = {nullptr, nullptr};
+  double st_t0 = 0, st_t1 = 0;
+  struct StepTime { long n = 0; double launch = 0, gpu = 0, wait = 0, total = 0; };
+  std::map<int, StepTime> st_sum;
+  int st_T = 0;
   ffmi_status forward(int k) {
     ffmi_status st = forward_launch(k);
     if (st != FFMI_OK) return st;
@@ -694,19 +736,31 @@ struct LlamaGPU : public ffmi_model {
   ffmi_status forward_launch(int k) {
     inflight = false;
     const int T = (int)ps.tokens.size();
+    if (step_timing) {
+      if (!st_ev[0]) {
+        FFMI_HIP(hipEventCreate(&st_ev[0]));
+        FFMI_HIP(hipEventCreate(&st_ev[1]));
+      }
+      st_t0 = now_us();
+      st_T = T;
+    }
     prof_this_step = prof_level == 1 && (prof_steps++ % prof_every) == 0;
     ffmi_batch_desc desc;
     ps.desc(&desc);
     // the embedding gather indexes the table by token id: reject bad ids on
     // the host instead of reading out of bounds on the device
+    // (a chained beam step's -1 - i: entry i of the previous slot's ids,
+    // themselves top-k picks in range)
+    const long prev_n = cur_slot > 0 ? (long)slot_results[cur_slot - 1] : 0;
     for (int t = 0; t < T; ++t)
-      FFMI_CHECK(desc.tokens[t].token_id >= 0 && desc.tokens[t].token_id < c.vocab_size,
+      FFMI_CHECK((desc.tokens[t].token_id >= 0 && desc.tokens[t].token_id < c.vocab_size) ||
+                     (desc.tokens[t].token_id < 0 && -1L - desc.tokens[t].token_id < prev_n),
                  FFMI_ERR_INVALID);
     size_t bytes = 0;
     ffmi_status st = ffmi::batch_stage(batch, &desc, &bytes);
     if (st != FFMI_OK) return st;
     if (T == 0) return FFMI_OK;
-    probs_h = reinterpret_cast<float *>(ids_h + (size_t)T * k);  // (also on graph replay)
+    probs_h = reinterpret_cast<float *>(ids_h + cur_slot * slot_ints() + (size_t)T * k);
     // graphed: small steps, and tree-verify steps of one work item per
     // request (a fixed shape while the batch is full: T = 168 for 8 requests
     // of 21 tree tokens); prefill blocks stay eager (one-off shapes)
@@ -718,7 +772,7 @@ struct LlamaGPU : public ffmi_model {
       const GraphKey key{T, batch->num_work, batch->num_commits, k, tree_parity,
                          batch->commit_overlap ? 1 : 0,
                          (batch->one_item_per_req ? 1 : 0) | (batch->lds_tail ? 2 : 0),
-                         batch->max_q, bytes};
+                         batch->max_q, cur_slot, bytes};
       auto it = graphs.find(key);
       if (it == graphs.end()) {
         if (graphs.size() >= 512) clear_graphs();
@@ -737,10 +791,16 @@ struct LlamaGPU : public ffmi_model {
         FFMI_HIP(ie);
         it = graphs.emplace(key, ex).first;
       }
+      if (step_timing) FFMI_HIP(hipEventRecord(st_ev[0], stream));
       FFMI_HIP(hipGraphLaunch(it->second, stream));
     } else {
+      if (step_timing) FFMI_HIP(hipEventRecord(st_ev[0], stream));
       st = enqueue(k, bytes, true);
       if (st != FFMI_OK) return st;
+    }
+    if (step_timing) {
+      FFMI_HIP(hipEventRecord(st_ev[1], stream));
+      st_t1 = now_us();
     }
     inflight = true;
     return FFMI_OK;
@@ -750,7 +810,19 @@ struct LlamaGPU : public ffmi_model {
     if (!inflight) return FFMI_OK;
     inflight = false;
     ffmi_status st;
+    const double tw = step_timing ? now_us() : 0;
     FFMI_HIP(hipStreamSynchronize(stream));
+    if (step_timing) {
+      const double te = now_us();
+      float ms = 0;
+      (void)hipEventElapsedTime(&ms, st_ev[0], st_ev[1]);
+      StepTime &q = st_sum[st_T];
+      q.n++;
+      q.launch += st_t1 - st_t0;
+      q.gpu += ms * 1e3;
+      q.wait += te - tw;
+      q.total += te - st_t0;
+    }
     // any attached transport (also under the RCCL path, whose chunks that fit
     // the exchange buffer still go over it) reports timeouts / errors here
     if ((peer || (o.comm && ffmi::comm_peer_attached(o.comm))) &&
@@ -828,7 +900,9 @@ struct LlamaGPU : public ffmi_model {
                                       h, T, H, eps, stream, packed,
                                       l == 0 ? ffmi::Partials() : down_part,
                                       l == 0 ? (blob_fetch ? batch->host : batch->dev) : nullptr,
-                                      l == 0 && blob_fetch ? batch->dev : nullptr, blob_bytes));
+                                      l == 0 && blob_fetch ? batch->dev : nullptr, blob_bytes,
+                                      cur_slot > 0 ? ids_dev + (size_t)(cur_slot - 1) * (slot_ints() / 2)
+                                                   : nullptr));
         // the staging is free for the next step once the fetch has read it
         if (l == 0 && blob_fetch && record_upload) FFMI_HIP(hipEventRecord(batch->uploaded, stream));
         prof_end(pr, NORM, (double)T * H * 2 * (l == 0 ? 3 : 4), 0);
@@ -922,6 +996,11 @@ struct LlamaGPU : public ffmi_model {
       if (dbg) TRY(dbg_gemm_out(FFMI_DBG_DOWN, l, proj, down_part, T));
     }
     const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
+    // (markers also between the tail's kernels: final norm, lm_head, sampling)
+    const bool tail_mark = marker_h == c.hidden && (!marker_t || T == marker_t);
+    auto mkt = [&]() {
+      if (tail_mark) (void)ffmi::launch_marker(mark_i++, stream);
+    };
     pr = prof_begin(ptail);
     if (fuse)  // res already holds the last residual add
       FFMI_HIP(ffmi::launch_rmsnorm(res, nullptr, final_norm, nullptr, h, T, H, eps, stream, packed));
@@ -929,6 +1008,7 @@ struct LlamaGPU : public ffmi_model {
       FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
                                     down_part));
     prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+    mkt();
     if (dbg) {
       TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers - 1, res, T));
       TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers, h, T));
@@ -937,9 +1017,11 @@ struct LlamaGPU : public ffmi_model {
     pr = prof_begin(ptail);
     TRY(ffmi_linear_ws(h, lm, logits, T, Vl, H, FFMI_EPI_NONE | XP, ws, ws_bytes, s));
     prof_end(pr, GEMM_LM_HEAD, gemm_bytes(T, Vl, Vl, H), 2.0 * T * Vl * H);
+    mkt();
     pr = prof_begin(ptail);
     TRY(enqueue_sampling(k, T));
     prof_end(pr, SAMPLING, (double)T * V * 2, 0);
+    mkt();
 #undef TRY
     return FFMI_OK;
   }
@@ -956,18 +1038,23 @@ struct LlamaGPU : public ffmi_model {
     // PCIe, visible after the stream synchronisation like a copy kernel's
     // stores), so a step needs no result-copy launch; FFMI_RESULT_COPY=1
     // keeps the device buffer + copy (A/B runs)
-    int32_t *ids_o = result_copy ? ids_d : ids_h;
+    int32_t *ids_o = result_copy ? ids_d : ids_h + cur_slot * slot_ints();
     float *probs_o = reinterpret_cast<float *>(ids_o + (size_t)T * k);
     if (Vl != V) {
       // sharded softmax / top-k: three record exchanges, then the merge
       TRY(ffmi_vocab_shard_topk(o.comm, logits, T, Vl, k, ids_o, probs_o, xch, s));
-    } else if (k == 1) {
-      TRY(ffmi_argmax(logits, T, V, ids_o, probs_o, s));
     } else {
-      TRY(ffmi_arg_topk(logits, T, V, k, ids_o, probs_o, s));
+      // the ids also to device memory: the next chained beam step's
+      // embedding gather reads them there
+      FFMI_CHECK(k >= 1 && k <= 4 && k <= V, FFMI_ERR_INVALID);
+      FFMI_HIP(ffmi::launch_argmax(logits, T, V, k, ids_o, probs_o, stream, topk_ws, topk_ws_bytes,
+                                   mode == FFMI_MODEL_BEAM
+                                       ? ids_dev + (size_t)cur_slot * (slot_ints() / 2)
+                                       : nullptr));
     }
     if (result_copy)
-      FFMI_HIP(hipMemcpyAsync(ids_h, ids_d, (size_t)T * k * 8, hipMemcpyDeviceToHost, stream));
+      FFMI_HIP(hipMemcpyAsync(ids_h + cur_slot * slot_ints(), ids_d, (size_t)T * k * 8,
+                              hipMemcpyDeviceToHost, stream));
 #undef TRY
     return FFMI_OK;
   }
@@ -976,6 +1063,7 @@ struct LlamaGPU : public ffmi_model {
     if (mode != FFMI_MODEL_INC) return FFMI_ERR_INVALID;
     FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
     pack_inc(bc, o.max_requests, slots, &ps);
+    cur_slot = 0;
     ffmi_status st = forward(1);
     if (st != FFMI_OK) return st;
     memcpy(ir->token_ids, ids_h, bc.num_tokens * sizeof(int32_t));
@@ -985,6 +1073,7 @@ struct LlamaGPU : public ffmi_model {
     if (mode != FFMI_MODEL_TREE) return FFMI_ERR_INVALID;
     FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
     pack_tree(bc, o.max_requests, slots, &ps);
+    cur_slot = 0;
     ffmi_status st = forward(1);
     if (st != FFMI_OK) return st;
     memcpy(ir->token_ids, ids_h, bc.num_tokens * sizeof(int32_t));
@@ -995,22 +1084,68 @@ struct LlamaGPU : public ffmi_model {
     if (st != FFMI_OK) return st;
     return beam_collect(ir);
   }
-  size_t beam_results = 0;  // results of the launched beam step (tokens x k)
   ffmi_status beam_launch(const BeamSearchBatchConfig &bc) override {
-    if (mode != FFMI_MODEL_BEAM) return FFMI_ERR_INVALID;
-    FFMI_CHECK(bc.num_tokens <= o.max_tokens, FFMI_ERR_INVALID);
-    pack_beam(bc, o.max_requests, slots, &ps);
-    const int k = ps.topk;
-    beam_results = (size_t)bc.num_tokens * k;
-    return forward_launch(k);
+    return beam_launch_chained(bc, 0);
   }
-  ffmi_status beam_collect(BeamInferenceResult *ir) override {
-    ffmi_status st = forward_finish();
-    if (st != FFMI_OK) return st;
-    const size_t n = beam_results;
-    memcpy(ir->token_ids, ids_h, n * sizeof(int32_t));
-    memcpy(ir->probs, probs_h, n * sizeof(float));
-    for (size_t i = 0; i < n; ++i) ir->parent_id[i] = 0;
+  ffmi_status beam_collect(BeamInferenceResult *ir) override { return beam_collect_chained(0, ir); }
+  // an unsharded SSM, not under debug capture
+  bool can_chain_beam() const override {
+    return chain_ok && mode == FFMI_MODEL_BEAM && o.tp_size == 1 && !dbg && !result_copy;
+  }
+  ffmi_status beam_launch_chained(const BeamSearchBatchConfig &bc, int slot) override {
+    if (mode != FFMI_MODEL_BEAM) return FFMI_ERR_INVALID;
+    FFMI_CHECK(bc.num_tokens <= o.max_tokens && slot >= 0 && slot < kChain, FFMI_ERR_INVALID);
+    FFMI_CHECK(slot == 0 || can_chain_beam(), FFMI_ERR_INVALID);
+    if (!chain_batch[slot]) {
+      ffmi_batch_dev *b = nullptr;
+      ffmi_status st = ffmi_batch_create((o.max_tokens + 15) & ~15, o.max_requests, &b);
+      if (st != FFMI_OK) return st;
+      chain_batch[slot] = b;
+    }
+    pack_beam(bc, o.max_requests, slots, &ps);
+    // a chained step's -1 - i (scheduler entry i of the previous slot) ->
+    // -1 - its [T][k] index, which the gather reads from device memory
+    for (auto &ti : ps.tokens)
+      if (ti.token_id < 0) {
+        const long i = -1L - ti.token_id;
+        FFMI_CHECK(slot > 0 && i < (long)slot_map[slot - 1].size(), FFMI_ERR_INVALID);
+        ti.token_id = -1 - slot_map[slot - 1][i];
+      }
+    const int k = ps.topk;
+    cur_slot = slot;
+    batch = chain_batch[slot];
+    slot_results[slot] = (size_t)bc.num_tokens * k;
+    beam_result_layout(bc, &slot_map[slot]);
+    ffmi_status st = forward_launch(k);
+    batch = chain_batch[0];
+    cur_slot = 0;
+    if (st == FFMI_OK) {
+      // (so that the scheduler can collect this slot while later ones run)
+      if (!slot_ev[slot]) FFMI_HIP(hipEventCreateWithFlags(&slot_ev[slot], hipEventDisableTiming));
+      FFMI_HIP(hipEventRecord(slot_ev[slot], stream));
+      last_slot = slot;
+    }
+    return st;
+  }
+  ffmi_status beam_collect_chained(int slot, BeamInferenceResult *ir) override {
+    FFMI_CHECK(slot >= 0 && slot < kChain, FFMI_ERR_INVALID);
+    if (slot < last_slot && slot_ev[slot]) {
+      // later slots still run: wait for this one only
+      FFMI_HIP(hipEventSynchronize(slot_ev[slot]));
+    } else {
+      ffmi_status st = forward_finish();  // (every launched step: one stream)
+      if (st != FFMI_OK) return st;
+      last_slot = -1;
+    }
+    const size_t n = slot_results[slot];
+    const int32_t *ids = ids_h + slot * slot_ints();
+    const float *pr = reinterpret_cast<const float *>(ids + n);
+    const std::vector<int> &map = slot_map[slot];
+    for (size_t i = 0; i < map.size(); ++i) {
+      ir->token_ids[i] = ids[map[i]];
+      ir->probs[i] = pr[map[i]];
+      ir->parent_id[i] = 0;
+    }
     return FFMI_OK;
   }
 };

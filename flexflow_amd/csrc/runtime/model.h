@@ -37,6 +37,14 @@ struct PackedStep {
 void pack_inc(const BatchConfig &bc, int max_requests, int slots, PackedStep *out);
 void pack_tree(const TreeVerifyBatchConfig &bc, int max_requests, int slots, PackedStep *out);
 void pack_beam(const BeamSearchBatchConfig &bc, int max_requests, int slots, PackedStep *out);
+// A beam step's results as the scheduler reads them (store_beam_metadata,
+// request_manager.cc:2217-2325): each token's top-w entries, w its request's
+// beam width, back to back in token order.  The step computes the top-k of
+// every token for k = beam_step_topk (the widest request) into [T][k]; map[i]
+// is the [T][k] index of scheduler entry i (the identity when every request
+// has the same width).
+int beam_step_topk(const BeamSearchBatchConfig &bc);
+void beam_result_layout(const BeamSearchBatchConfig &bc, std::vector<int> *map);
 
 }  // namespace ffmi
 
@@ -64,6 +72,31 @@ struct ffmi_model {
     return run_beam(*bc, ir);
   }
   const ffmi::BeamSearchBatchConfig *pending_beam = nullptr;
+  // Chained beam steps (serve_spec_infer): the 8 beam steps of a speculation
+  // phase are launched back to back without waiting for results.  Step
+  // `slot` > 0 carries token id -1 - i where its token is entry i of step
+  // slot - 1's top-k ids (the device fills it in); the results of every slot
+  // are kept until the next phase.  The scheduler's state does not depend on
+  // the token values beyond those ids, so it stages all 8 steps up front and
+  // replays its bookkeeping once the results are in (request_manager.cpp).
+  virtual bool can_chain_beam() const { return false; }
+  virtual ffmi_status beam_launch_chained(const ffmi::BeamSearchBatchConfig &bc, int slot) {
+    (void)bc;
+    (void)slot;
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  virtual ffmi_status beam_collect_chained(int slot, ffmi::BeamInferenceResult *ir) {
+    (void)slot;
+    (void)ir;
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  // tokens one step can hold (-1: unknown), checked by serve_spec_infer
+  // against the largest batch the scheduler can build for an SSM
+  virtual int token_capacity() const { return -1; }
+  // a TP-sharded model: its steps run collectives on a communicator, so two
+  // such models' steps must not be in flight at once (their collectives
+  // could pair up across ranks in different orders)
+  virtual bool uses_collectives() const { return false; }
   virtual ffmi_status set_profiling(int level) {
     (void)level;
     return FFMI_ERR_UNSUPPORTED;

@@ -133,18 +133,32 @@ void pack_tree(const TreeVerifyBatchConfig &bc, int max_requests, int slots, Pac
   build_work(ps);
 }
 
+int beam_step_topk(const BeamSearchBatchConfig &bc) {
+  int k = 1;
+  for (int t = 0; t < bc.num_tokens; ++t)
+    k = std::max(k, bc.beamRequestsInfo[bc.tokensInfo[t].request_index].beam_size);
+  return k;
+}
+
+void beam_result_layout(const BeamSearchBatchConfig &bc, std::vector<int> *map) {
+  const int k = beam_step_topk(bc);
+  map->clear();
+  for (int t = 0; t < bc.num_tokens; ++t) {
+    const int w = bc.beamRequestsInfo[bc.tokensInfo[t].request_index].beam_size;
+    for (int j = 0; j < w && j < k; ++j) map->push_back(t * k + j);
+  }
+}
+
 void pack_beam(const BeamSearchBatchConfig &bc, int max_requests, int slots,
                PackedStep *ps) {
   ps->tokens.resize(bc.num_tokens);
   ps->commits.clear();
   copy_masks(bc, max_requests, ps);
-  // ArgTopK takes its k from the first active request (arg_topk.cu:403-420)
-  ps->topk = 1;
-  for (int r = 0; r < BatchConfig::MAX_NUM_REQUESTS && r < max_requests; ++r)
-    if (!bc.request_completed[r]) {
-      ps->topk = bc.beamRequestsInfo[r].beam_size;
-      break;
-    }
+  // the top-k of every token for the widest request of the step (the
+  // reference's ArgTopK computes MAX_BEAM_WIDTH for every token and asserts
+  // that all requests but the last share one width, arg_topk.cu:403-420);
+  // beam_result_layout hands each request its own width's entries
+  ps->topk = beam_step_topk(bc);
   for (int t = 0; t < bc.num_tokens; ++t) {
     const auto &tk = bc.tokensInfo[t];
     const int r = tk.request_index;

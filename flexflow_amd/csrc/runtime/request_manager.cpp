@@ -18,9 +18,13 @@
 #include <assert.h>
 #include <stdio.h>
 
+#include <stdlib.h>
+#include <string.h>
+
 #include <algorithm>
 #include <chrono>
 #include <map>
+#include <memory>
 
 void ffmi_set_last_error(const char *msg, const char *file, int line);  // api.cpp
 
@@ -958,14 +962,18 @@ void RequestManager::tree_bitmask(const std::vector<int> &parent, int n,
 // depth-first serialisation traverse_beam_tree no longer produces).  The union
 // is emitted in layer order (depth, then first-seen: SSM 0's nodes, then new
 // nodes of SSM 1, ...), the order the verify step, its bitmask and the commit
-// lists use, and is cut to max_spec_tree_token_num nodes (<= 64, the
-// bitmask's width): a layer-order prefix, so every kept node keeps its
+// lists use, and is cut to the root + max_spec_tree_token_num nodes (<= 64,
+// the bitmask's width): a layer-order prefix, so every kept node keeps its
 // ancestors.
 std::vector<RequestManager::TokenDepth> RequestManager::merge_dfs_trees(
     const std::vector<std::vector<TokenDepth>> &trees, int root_depth, RequestGuid guid) {
   (void)root_depth;
   assert(!trees.empty());
-  const int cap = std::max(1, std::min(max_spec_tree_token_num,
+  // root + max_spec_tree_token_num nodes: the root's KV slot lies in the
+  // committed range, so the models' tail of max_spec_tree_token_num slots
+  // per request holds that many nodes below it (the reference places a
+  // widths (1,1,3) tree of 21 nodes whole under its default budget of 20)
+  const int cap = std::max(1, std::min(max_spec_tree_token_num + 1,
                                        (int)BatchConfig::MAX_SPEC_TREE_TOKEN_NUM));
   if (trees.size() == 1) {
     // (cut to the cap like a merged tree: a tree larger than the models' KV
@@ -1065,6 +1073,166 @@ ffmi_status RequestManager::serve_incr_decoding(ffmi_model *llm) {
   return st;
 }
 
+// Does a beam batch staged from placeholder results (`spec`: the previous
+// step's top-k id i appears as token id -1 - i) describe the batch built from
+// the real results (`real`)?  Everything but those token ids must agree, and
+// each placeholder must name the real id.
+static bool same_beam_batch(const BeamSearchBatchConfig &spec, const BeamSearchBatchConfig &real,
+                            const BeamInferenceResult &prev, int max_requests) {
+  if (spec.num_tokens != real.num_tokens || spec.model_id != real.model_id) return false;
+  for (int t = 0; t < real.num_tokens; ++t) {
+    const auto &a = spec.tokensInfo[t], &b = real.tokensInfo[t];
+    if (a.request_index != b.request_index || a.abs_depth_in_request != b.abs_depth_in_request ||
+        spec.beamTokenInfo[t].sub_request_index != real.beamTokenInfo[t].sub_request_index)
+      return false;
+    const int id = a.token_id < 0 ? prev.token_ids[-1 - a.token_id] : a.token_id;
+    if (id != b.token_id) return false;
+  }
+  for (int r = 0; r < max_requests && r < BatchConfig::MAX_NUM_REQUESTS; ++r) {
+    if (spec.request_completed[r] != real.request_completed[r] ||
+        spec.request_running[r] != real.request_running[r])
+      return false;
+    if (real.request_completed[r]) continue;
+    const auto &a = spec.requestsInfo[r], &b = real.requestsInfo[r];
+    if (a.first_token_depth_in_request != b.first_token_depth_in_request ||
+        a.first_token_offset_in_batch != b.first_token_offset_in_batch ||
+        a.num_tokens_in_batch != b.num_tokens_in_batch || a.prompt_phase != b.prompt_phase)
+      return false;
+    const auto &ma = spec.causalMask[r], &mb = real.causalMask[r];
+    if (ma.non_tree_cache_size != mb.non_tree_cache_size || ma.tree_size != mb.tree_size ||
+        ma.this_layer_size != mb.this_layer_size || ma.prompt_size != mb.prompt_size ||
+        memcmp(ma.mask, mb.mask, sizeof ma.mask) != 0)
+      return false;
+    const auto &ba = spec.beamRequestsInfo[r], &bb = real.beamRequestsInfo[r];
+    if (ba.beam_size != bb.beam_size || ba.current_depth != bb.current_depth ||
+        ba.max_depth != bb.max_depth || ba.sub_request_num != bb.sub_request_num)
+      return false;
+  }
+  return true;
+}
+
+// The speculation phase with chained beam steps.  What a beam step's batch
+// holds -- sizes, positions, KV slots, bitmasks -- follows from the tree
+// widths, depths and prompt lengths; only its generation tokens' ids come from
+// the previous step's results (B.tokens, store_beam_metadata /
+// update_beam_metadata).  So the 8 steps of each SSM are prepared up front
+// from placeholder results whose entry i reads -1 - i, and launched back to
+// back: the device puts the previous step's top-k id i in place of -1 - i
+// (the embedding gather), with no host round trip between steps.  The
+// scheduler state those placeholder preparations touched is then restored and
+// the same prepare_next_batch_beam calls are replayed, in the order the
+// stepwise loop makes them, on the real results -- so beam trees, counters and
+// the final batches are exactly the stepwise ones -- and every staged batch is
+// checked against the replayed one (same_beam_batch; a mismatch is an error,
+// never a silent divergence).
+ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchConfig> *beam_vec,
+                                                  BeamInferenceResult *beam_ir) {
+  const size_t n = ssm_models.size();
+  const int D = BeamSearchBatchConfig::MAX_BEAM_DEPTH;
+  const double ts = now_us();
+  double prep_us = 0, t_last = ts;
+  ffmi_status st = FFMI_OK;
+  // step 0 of every SSM (its tokens are known)
+  size_t launched0 = 0;
+  for (size_t s = 0; s < n && st == FFMI_OK; ++s) {
+    st = ssm_models[s]->beam_launch_chained((*beam_vec)[s], 0);
+    if (st == FFMI_OK) ++launched0;
+  }
+  // the state prepare_next_batch_beam writes, saved for the replay
+  struct Saved {
+    std::vector<Request::BeamTree> trees;
+    int ssm_cache_size;
+  };
+  std::map<RequestGuid, Saved> saved;
+  for (const auto &kv : all_requests)
+    saved[kv.first] = Saved{kv.second.beam_trees, kv.second.ssm_cache_size};
+  std::map<RequestGuid, int> saved_steps;
+  for (const auto &kv : profiling_requests) saved_steps[kv.first] = kv.second.ssm_decoding_steps;
+  // steps 1 .. D-1 prepared from placeholders while step 0 runs: spec[s * D + d]
+  std::vector<BeamSearchBatchConfig> &spec = chain_spec;
+  spec.resize(n * D);
+  if (!chain_ph) {
+    chain_ph.reset(new BeamInferenceResult());
+    for (int i = 0;
+         i < BatchConfig::MAX_NUM_TOKENS * BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES; ++i) {
+      chain_ph->token_ids[i] = -1 - i;
+      chain_ph->probs[i] = 1.0f;
+      chain_ph->parent_id[i] = 0;
+    }
+  }
+  // a placeholder must name an entry the previous step produces (its
+  // tokens' top-w entries, beam_result_layout); otherwise the phase runs
+  // step by step
+  std::vector<int> layout;
+  auto results_of = [&](const BeamSearchBatchConfig &bc) -> long {
+    beam_result_layout(bc, &layout);
+    return (long)layout.size();
+  };
+  bool chainable = st == FFMI_OK;
+  const double tp0 = now_us();
+  for (size_t s = 0; s < n && chainable; ++s) {
+    spec[s * D] = (*beam_vec)[s];
+    for (int d = 1; d < D && chainable; ++d) {
+      spec[s * D + d] = prepare_next_batch_beam(spec[s * D + d - 1], *chain_ph);
+      const long have = results_of(spec[s * D + d - 1]);
+      const BeamSearchBatchConfig &b = spec[s * D + d];
+      for (int t = 0; t < b.num_tokens; ++t)
+        if (b.tokensInfo[t].token_id < 0 && -1L - b.tokensInfo[t].token_id >= have)
+          chainable = false;
+    }
+  }
+  for (auto &kv : all_requests) {  // restore
+    auto it = saved.find(kv.first);
+    if (it == saved.end()) continue;
+    kv.second.beam_trees = it->second.trees;
+    kv.second.ssm_cache_size = it->second.ssm_cache_size;
+  }
+  for (auto &kv : profiling_requests) {
+    auto it = saved_steps.find(kv.first);
+    if (it != saved_steps.end()) kv.second.ssm_decoding_steps = it->second;
+  }
+  prep_us += now_us() - tp0;
+  // launch steps 1 .. D-1 back to back (chainable), or nothing more yet
+  if (chainable) stats.ssm_phases_chained++;
+  size_t launched = launched0;
+  for (int d = 1; d < D && chainable && st == FFMI_OK; ++d)
+    for (size_t s = 0; s < n && st == FFMI_OK; ++s) {
+      st = ssm_models[s]->beam_launch_chained(spec[s * D + d], d);
+      if (st == FFMI_OK) ++launched;
+    }
+  // collect in the stepwise loop's order, replaying the bookkeeping on the
+  // real results; unchained: collect, prepare, launch the next step (slot 0)
+  for (int d = 0; d < D; ++d)
+    for (size_t s = 0; s < n; ++s) {
+      const bool was_launched = chainable ? (size_t)d * n + s < launched
+                                          : (d == 0 ? s < launched0 : st == FFMI_OK);
+      if (!was_launched) continue;
+      const ffmi_status cs = ssm_models[s]->beam_collect_chained(chainable ? d : 0, beam_ir);
+      t_last = now_us();
+      if (st == FFMI_OK) st = cs;
+      if (st != FFMI_OK) continue;  // (collect the rest: nothing left in flight)
+      stats.ssm_steps++;
+      const double tp = now_us();
+      (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+      if (chainable && d + 1 < D &&
+          !same_beam_batch(spec[s * D + d + 1], (*beam_vec)[s], *beam_ir, max_requests_per_batch)) {
+        ffmi_set_last_error("chained SSM beam steps: a staged batch differs from the one its "
+                            "results give (FFMI_SSM_CHAIN=0 runs the steps one by one)",
+                            __FILE__, __LINE__);
+        st = FFMI_ERR_INVALID;
+      }
+      prep_us += now_us() - tp;
+      if (!chainable && st == FFMI_OK && d + 1 < D)
+        st = ssm_models[s]->beam_launch_chained((*beam_vec)[s], 0);
+    }
+  // first launch to last result: the staging and the replay of every step
+  // but the last overlap the device's work; what follows the last result is
+  // host scheduling, as in the stepwise loop
+  (void)prep_us;
+  stats.ssm_us += t_last - ts;
+  return st;
+}
+
 // request_manager.cc:3083-3173
 ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   if (!llm) return FFMI_ERR_INVALID;
@@ -1075,6 +1243,47 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
                         __FILE__, __LINE__);
     return FFMI_ERR_UNSUPPORTED;
   }
+  // every SSM step must fit its model: an init batch holds every running
+  // request's verified tokens (up to MAX_BEAM_DEPTH + 1 each) or prompt
+  // chunks up to max_tokens_per_batch, a beam step every request's beams
+  // (up to MAX_SPECULATIVE_TREE_BRANCHES each) or prompt chunks up to the
+  // same budget.  Checked here rather than failing partway through a serve
+  {
+    const int need = std::max(max_tokens_per_batch,
+                              max_requests_per_batch *
+                                  std::max(BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1,
+                                           (int)BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES));
+    for (size_t s = 0; s < ssm_models.size(); ++s) {
+      const int cap = ssm_models[s]->token_capacity();
+      if (cap >= 0 && cap < need) {
+        char msg[256];
+        snprintf(msg, sizeof msg,
+                 "SpecInfer: SSM %zu holds %d tokens per step, the scheduler can build %d "
+                 "(max(max_tokens_per_batch, max_requests x %d)): create it with max_tokens >= %d",
+                 s, cap, need,
+                 std::max(BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1,
+                          (int)BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES),
+                 need);
+        ffmi_set_last_error(msg, __FILE__, __LINE__);
+        return FFMI_ERR_INVALID;
+      }
+    }
+  }
+  // requests registered before the last SSM was: one beam tree per SSM
+  for (auto &kv : all_requests)
+    if (kv.second.beam_trees.size() < ssm_models.size())
+      kv.second.beam_trees.resize(ssm_models.size());
+  for (auto &r : pending_infr_request_queue)
+    if (r.beam_trees.size() < ssm_models.size()) r.beam_trees.resize(ssm_models.size());
+  // SSMs whose steps run collectives (TP-sharded) are stepped one at a time:
+  // their steps' all-reduces must reach every rank in the same order
+  bool overlap_ssms = true;
+  for (auto *m : ssm_models)
+    if (m->uses_collectives()) overlap_ssms = false;
+  // chained beam steps where every SSM supports them (FFMI_SSM_CHAIN=0: off)
+  bool chain = overlap_ssms && !(getenv("FFMI_SSM_CHAIN") && atoi(getenv("FFMI_SSM_CHAIN")) == 0);
+  for (auto *m : ssm_models)
+    if (!m->can_chain_beam()) chain = false;
   apply_limits();
   stats = Stats();
   const double t0 = now_us();
@@ -1105,16 +1314,32 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
     // is collected and its next batch prepared, while the other SSMs' steps
     // d are still running (identical batches and results: each SSM's chain
     // of steps is unchanged)
-    {
+    if (chain) {
+      st = run_ssm_phase_chained(beam_vec, beam_ir);
+    } else {
       const size_t n = ssm_models.size();
       const double ts = now_us();
       double prep_us = 0;
       std::vector<bool> inflight(n, false);
-      for (size_t s = 0; s < n && st == FFMI_OK; s++) {
+      if (!overlap_ssms) {
+        // one step in flight at a time, SSM by SSM (the reference's order)
+        for (size_t s = 0; s < n && st == FFMI_OK; s++)
+          for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && st == FFMI_OK;
+               depth++) {
+            st = ssm_models[s]->beam_launch((*beam_vec)[s]);
+            if (st == FFMI_OK) st = ssm_models[s]->beam_collect(beam_ir);
+            if (st != FFMI_OK) break;
+            stats.ssm_steps++;
+            const double tp = now_us();
+            (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+            prep_us += now_us() - tp;
+          }
+      }
+      for (size_t s = 0; s < n && st == FFMI_OK && overlap_ssms; s++) {
         st = ssm_models[s]->beam_launch((*beam_vec)[s]);
         inflight[s] = st == FFMI_OK;
       }
-      for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH; depth++) {
+      for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && overlap_ssms; depth++) {
         for (size_t s = 0; s < n; s++) {
           if (!inflight[s]) continue;
           inflight[s] = false;

@@ -9,6 +9,7 @@
 #pragma once
 #include <deque>
 #include <map>
+#include <memory>
 #include <string>
 #include <unordered_map>
 #include <utility>
@@ -139,6 +140,11 @@ class RequestManager {
 
   ffmi_status serve_incr_decoding(ffmi_model *llm);
   ffmi_status serve_spec_infer(ffmi_model *llm);
+  // the speculation phase as chained beam steps (model.h): every SSM's
+  // MAX_BEAM_DEPTH steps staged and launched up front, the bookkeeping
+  // replayed on the results (identical batches and trees)
+  ffmi_status run_ssm_phase_chained(std::vector<BeamSearchBatchConfig> *beam_vec,
+                                    BeamInferenceResult *beam_ir);
 
   bool all_done() const;
   const GenerationResult *get_generation_result(RequestGuid guid) const;
@@ -156,6 +162,7 @@ class RequestManager {
     long request_verifies = 0;
     double wall_us = 0;
     double llm_us = 0, ssm_us = 0;  // wall time inside the model steps (incl. sync)
+    long ssm_phases_chained = 0;
   } stats;
 
  private:
@@ -191,6 +198,8 @@ class RequestManager {
   std::vector<ffmi_model *> ssm_models;
   std::map<RequestGuid, ProfileInfo> profiling_requests;
   size_t num_processed_requests = 0;
+  std::vector<BeamSearchBatchConfig> chain_spec;  // staged chained beam batches
+  std::unique_ptr<BeamInferenceResult> chain_ph;   // placeholder results (-1 - i)
 };
 
 double now_us();

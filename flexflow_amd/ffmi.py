@@ -118,7 +118,8 @@ class OpStat(ctypes.Structure):
 class ServeStats(ctypes.Structure):
     _fields_ = [("llm_steps", c_long), ("ssm_steps", c_long), ("tokens_committed", c_long),
                 ("tree_tokens_verified", c_long), ("request_verifies", c_long),
-                ("wall_us", c_double), ("llm_us", c_double), ("ssm_us", c_double)]
+                ("wall_us", c_double), ("llm_us", c_double), ("ssm_us", c_double),
+                ("ssm_phases_chained", c_long)]
 
 
 # name -> (restype, argtypes); every symbol declared in include/ffmi.h
@@ -165,6 +166,9 @@ SIGNATURES = {
     "ffmi_silu_mul": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ffmi_argmax": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),
     "ffmi_arg_topk": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p]),
+    "ffmi_arg_topk_workspace_bytes": (c_size_t, [c_int]),
+    "ffmi_arg_topk_ws": (c_int, [c_void_p, c_int, c_int, c_int, c_void_p, c_void_p, c_void_p,
+                                 c_size_t, c_void_p]),
     "ffmi_fill_weight": (c_int, [c_void_p, c_size_t, ctypes.c_char_p, c_uint64, c_int, c_void_p]),
     "ffmi_model_create": (c_int, [ctypes.POINTER(LlamaConfig), ctypes.POINTER(ModelOpts),
                                   ctypes.POINTER(c_void_p)]),
@@ -209,6 +213,7 @@ SIGNATURES = {
 TEST_SIGNATURES = {
     "ffmi_test_hash_model_create": (c_int, [c_int, c_int, c_int, c_int, c_int, c_uint64, c_int,
                                             ctypes.POINTER(c_void_p)]),
+    "ffmi_test_hash_model_set_capacity": (c_int, [c_void_p, c_int]),
 }
 TEST_LIB_PATH = os.path.join(os.path.dirname(LIB_PATH), "libffmi_testmodel.so")
 

@@ -97,7 +97,7 @@ class HashModel(Model):
     """Scheduler test double (CPU only, see ffmi_test_hash_model_create)."""
 
     def __init__(self, vocab=1000, mode="inc", *, max_requests=8, max_seq_len=512,
-                 max_tree_tokens=23, salt=0, disagree_pct=0):
+                 max_tree_tokens=23, salt=0, disagree_pct=0, max_tokens=None):
         self.mode = mode
         h = ctypes.c_void_p()
         F.check(F.test_lib().ffmi_test_hash_model_create(vocab, self.MODES[mode], max_requests,
@@ -105,6 +105,8 @@ class HashModel(Model):
                                                     disagree_pct, ctypes.byref(h)),
                 "hash model")
         self.handle = h
+        if max_tokens is not None:  # a GPU model's token capacity per step
+            F.check(F.test_lib().ffmi_test_hash_model_set_capacity(h, max_tokens), "capacity")
 
 
 class Comm:

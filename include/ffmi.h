@@ -290,6 +290,16 @@ ffmi_status ffmi_argmax(const void *logits, int T, int V, int32_t *ids,
 /* softmax + ArgTopK (arg_topk.cu:339-448), k <= 4, sorted, lower index on ties */
 ffmi_status ffmi_arg_topk(const void *logits, int T, int V, int k, int32_t *ids,
                           float *probs, ffmi_stream stream);
+/* the same with a device workspace: rows of a small batch (the SSM's beam
+ * steps, decode) are split over several workgroups that each sum 1/G of the
+ * row's exp terms, identical results.  `workspace` holds
+ * ffmi_arg_topk_workspace_bytes(T) bytes, zero-filled by the caller once
+ * (the call leaves it zeroed); one workspace per stream in flight.  NULL or
+ * too small: the one-workgroup-per-row form (ffmi_arg_topk). */
+size_t ffmi_arg_topk_workspace_bytes(int T);
+ffmi_status ffmi_arg_topk_ws(const void *logits, int T, int V, int k, int32_t *ids,
+                             float *probs, void *workspace, size_t workspace_bytes,
+                             ffmi_stream stream);
 /* DT_FLOAT twins (--use-full-precision, kernels/f32.hip): RMSNorm /
  * ResidualRMSNorm (sum of squares in fp64, rounded once; fp32 residual add),
  * SigmoidSiluMulti, softmax + arg-top-k on fp32 probabilities (k <= 4, lowest
@@ -513,6 +523,7 @@ typedef struct {
   long request_verifies; /* (request, verify step) pairs that committed tokens */
   double wall_us;
   double llm_us, ssm_us; /* wall time inside LLM / SSM steps; the rest is host scheduling */
+  long ssm_phases_chained; /* speculation phases run as chained beam steps (FFMI_SSM_CHAIN) */
 } ffmi_serve_stats;
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 

@@ -14,6 +14,10 @@ extern "C" {
 ffmi_status ffmi_test_hash_model_create(int vocab, int mode, int max_requests,
                                         int max_seq, int max_tree, uint64_t salt,
                                         int disagree_pct, ffmi_model **out);
+/* Give the hash model a token capacity per step, as a GPU model's
+ * max_tokens: larger steps fail with FFMI_ERR_INVALID, and the scheduler's
+ * up-front SSM capacity check sees it.  TEST USE ONLY. */
+ffmi_status ffmi_test_hash_model_set_capacity(ffmi_model *m, int max_tokens);
 
 #ifdef __cplusplus
 }

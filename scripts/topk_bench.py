@@ -27,4 +27,16 @@ for T, V, k in [(24, 32000, 3), (24, 31999, 3), (168, 32000, 1), (8, 32000, 1), 
     n = 300
     for _ in range(n):
         L.ffmi_arg_topk(x.ptr, T, V, k, ids.ptr, pr.ptr, None)
-    print(f"T={T} V={V} k={k}: {tm.stop() * 1e3 / n:.2f} us per launch", flush=True)
+    t1 = tm.stop() * 1e3 / n
+    # the split-row form (the model's: a zeroed workspace)
+    nb = int(L.ffmi_arg_topk_workspace_bytes(T))
+    ws = Buf(np.zeros(nb // 4, np.uint32))
+    for _ in range(5):
+        F.check(L.ffmi_arg_topk_ws(x.ptr, T, V, k, ids.ptr, pr.ptr, ws.ptr, nb, None))
+    tm = Timer()
+    tm.start()
+    for _ in range(n):
+        L.ffmi_arg_topk_ws(x.ptr, T, V, k, ids.ptr, pr.ptr, ws.ptr, nb, None)
+    t2 = tm.stop() * 1e3 / n
+    print(f"T={T} V={V} k={k}: {t1:.2f} us per launch (one workgroup per row), "
+          f"{t2:.2f} us (split rows)", flush=True)

@@ -29,7 +29,7 @@ def test_test_doubles_live_outside_the_product_library():
     prod = ctypes.CDLL(F.LIB_PATH)
     test = ctypes.CDLL(F.TEST_LIB_PATH)
     names = declared_functions("ffmi_test.h")
-    assert names == ["ffmi_test_hash_model_create"]
+    assert names == ["ffmi_test_hash_model_create", "ffmi_test_hash_model_set_capacity"]
     for n in names:
         assert hasattr(test, n) and not hasattr(prod, n), n
     assert set(names) <= set(F.TEST_SIGNATURES)

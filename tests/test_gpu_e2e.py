@@ -129,6 +129,56 @@ def test_graph_replay_equals_eager(monkeypatch, ssm):
         assert with_graphs[0] == with_graphs[1]  # SpecInfer == incr decoding
 
 
+@pytest.mark.parametrize("case", ["small", "same", "two_ssms", "queued", "eager"])
+def test_chained_ssm_steps_equal_stepwise(monkeypatch, case):
+    """The speculation phase as chained beam steps (8 steps staged up front
+    and launched back to back; each step's embedding gather takes its tokens
+    from the previous step's top-k ids in device memory) against the stepwise
+    loop (FFMI_SSM_CHAIN=0): the same kernels on the same inputs, so the SSM
+    results, trees, verify batches and tokens must be IDENTICAL, and so must
+    every step count.  Cases: the small SSM, SSM == LLM weights (long accepted
+    paths), two SSMs with merged trees, more requests than slots (prompts
+    loading beside running requests), and eager steps (FFMI_NO_GRAPHS)."""
+    cfg, seed = LLM_CFG, 41
+    n, batch = (8, 4) if case == "queued" else (4, 4)
+    ps = prompts(n, cfg["vocab_size"], 5, 40, seed)
+    if case == "eager":
+        monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
+
+    def run(chain):
+        monkeypatch.setenv("FFMI_SSM_CHAIN", "1" if chain else "0")
+        vt = 64 + 23 * batch
+        ext = fa.ffmi.SPEC_EXT_MULTI_SSM if case == "two_ssms" else 0
+        rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=64,
+                               max_sequence_length=128, spec_tree_width=(1, 1, 3),
+                               max_spec_tree_token_num=23, spec_extensions=ext)
+        llm = fa.Model(cfg, "tree", max_requests=batch, max_tokens=vt, max_seq_len=128,
+                       max_tree_tokens=23, weight_seed=seed)
+        drafts = [(SSM_CFG, 5)] if case != "same" else [(cfg, seed)]
+        if case == "two_ssms":
+            drafts.append((SSM_CFG, 6))
+        models = [fa.Model(c, "beam", max_requests=batch, max_tokens=vt, max_seq_len=128,
+                           max_tree_tokens=23, weight_seed=sd) for c, sd in drafts]
+        for m in models:
+            rm.register_ssm_model(m)
+        res = fa.generate(rm, llm, ps, max_length=80, spec=True)
+        st = rm.stats()
+        out = [r.output_tokens for r in res], {
+            f: getattr(st, f) for f in ("llm_steps", "ssm_steps", "tokens_committed",
+                                        "tree_tokens_verified", "request_verifies")}
+        llm.close()
+        for m in models:
+            m.close()
+        return out, st.ssm_phases_chained
+
+    (toks0, st0), ch0 = run(False)
+    (toks1, st1), ch1 = run(True)
+    assert ch0 == 0 and ch1 > 0
+    assert toks1 == toks0
+    assert st1 == st0
+    report("chained_ssm_steps", case=case, phases_chained=ch1, **st1)
+
+
 def test_incr_decoding_matches_golden_fixture_model():
     # the HF-pinned fixture model (oracle fp32 == HF greedy); GPU fp16 vs oracle fp16
     cfg, g = O.load_golden("tiny_d128")

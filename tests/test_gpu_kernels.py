@@ -433,6 +433,97 @@ def test_softmax_topk_random_shapes_exact(seed):
     np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
 
 
+class TopkWs:
+    """A zeroed ffmi_arg_topk_ws workspace for up to Tmax rows (the model's
+    split-row top-k); `left_zero` checks the calls re-armed every counter."""
+
+    def __init__(self, Tmax):
+        self.nbytes = int(L.ffmi_arg_topk_workspace_bytes(Tmax))
+        self.buf = Buf(np.zeros(self.nbytes // 4, np.uint32))
+
+    def __call__(self, lb, T, V, k, ids, pr):
+        F.check(L.ffmi_arg_topk_ws(lb.ptr, T, V, k, ids.ptr, pr.ptr, self.buf.ptr, self.nbytes,
+                                   None), (T, V, k))
+
+    def counters_zero(self, T):
+        return not self.buf.get()[:T].any()
+
+
+@pytest.mark.parametrize("T", [1, 5, 8, 16, 17, 24, 32, 33, 64, 65, 100, 128])
+@pytest.mark.parametrize("V", [4104, 8000, 16000, 32000])
+def test_softmax_topk_split_rows_exact(T, V):
+    """The split-row form (ffmi_arg_topk_ws: T <= 128 rows over 2-16
+    workgroups each, chosen by T; the last workgroup of a row to publish its
+    partial sum finishes the row) against the oracle, bit-exact: random rows
+    at several scales, planted exact ties across the row, a flat row (more
+    candidates than the LDS list), repeated launches on one workspace (the
+    per-row counters must be re-armed), k 1-4."""
+    rng = np.random.default_rng(T * 100003 + V)
+    logits = f16(rng.standard_normal((T, V)) * rng.choice([0.05, 1.0, 3.0], size=(T, 1)))
+    logits[0, :] = f16(0.25)  # flat: every logit a candidate
+    for t in range(1, min(T, 4)):
+        m = f16(float(np.abs(logits[t]).max()) + 1.0)
+        logits[t, rng.choice(V, size=3, replace=False)] = m
+    lb = Buf(logits)
+    ws = TopkWs(128)
+    for k in (1, 2, 3, 4):
+        rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+        for _ in range(2):
+            ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+            ws(lb, T, V, k, ids, pr)
+            assert np.array_equal(ids.get(), rid.reshape(T, k)), (k, np.argwhere(ids.get() != rid.reshape(T, k))[:4])
+            np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
+        assert ws.counters_zero(T)
+    assert ids.get()[0].tolist() == list(range(4))
+
+
+def test_softmax_topk_split_one_workspace_many_shapes():
+    """One workspace for every step size, as the model keeps it: the row
+    counters sit at a fixed offset, so a step's partial sums never land on
+    the counters of a later step with more rows (round 6: they did, and the
+    next step found no last workgroup -- stale ids)."""
+    rng = np.random.default_rng(31337)
+    ws = TopkWs(128)
+    for T in (40, 100, 8, 128, 33, 17, 64, 1, 120, 24, 24, 65, 9):
+        V = 32000
+        logits = f16(rng.standard_normal((T, V)) * 2.0)
+        lb = Buf(logits)
+        k = int(rng.integers(1, 5))
+        ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+        ws(lb, T, V, k, ids, pr)
+        rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+        assert np.array_equal(ids.get(), rid.reshape(T, k)), T
+        np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
+        assert ws.counters_zero(128), T
+
+
+@pytest.mark.parametrize("seed", range(6 * RS))
+def test_softmax_topk_split_random_exact(seed):
+    """The split-row form at random shapes and scales (T 1-128, V a multiple
+    of 8 up to 32768, planted ties), bit-exact against the oracle and against
+    the one-workgroup form."""
+    rng = np.random.default_rng(4242 + OFF + seed)
+    T = int(rng.integers(1, 129))
+    V = 8 * int(rng.integers(8, 4097))
+    scale = float(rng.choice([1e-3, 0.05, 1.0, 3.0, 8.0]))
+    logits = f16(rng.standard_normal((T, V)) * scale)
+    for t in rng.choice(T, size=min(T, 4), replace=False):
+        m = f16(float(np.abs(logits[t]).max()) + 1.0)
+        logits[t, rng.choice(V, size=int(rng.integers(2, 6)), replace=False)] = m
+    lb = Buf(logits)
+    k = int(rng.integers(1, 5))
+    ws = TopkWs(T)
+    ids, pr = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+    ws(lb, T, V, k, ids, pr)
+    ids1, pr1 = Buf.empty((T, k), np.int32), Buf.empty((T, k), np.float32)
+    F.check(L.ffmi_arg_topk(lb.ptr, T, V, k, ids1.ptr, pr1.ptr, None))
+    rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
+    assert np.array_equal(ids.get(), rid.reshape(T, k)), (T, V, k, scale)
+    np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
+    assert np.array_equal(ids.get(), ids1.get()) and np.array_equal(pr.get(), pr1.get())
+    assert ws.counters_zero(T)
+
+
 @pytest.mark.parametrize("seed", range(8 * RS))
 def test_rmsnorm_random_shapes(seed):
     """RMSNorm / residual RMSNorm at random T (1-1100) and H (multiple of 8

@@ -271,6 +271,100 @@ def test_multi_ssm_chunked_prompts_and_queueing(tree_tokens):
     assert st.ssm_steps > 0
 
 
+def test_spec_infer_verifies_root_plus_budget_nodes():
+    """max_spec_tree_token_num counts the tree's nodes BELOW the root: widths
+    (1,1,3) over 8 beam steps grow 1 + 1 + 1 + 3 x 6 = 21 nodes with the root,
+    and under the reference's default llama budget of 20 the reference
+    verifies them all (the root's KV slot is in the committed range, so the
+    models' tail of max_spec_tree_token_num slots holds the 20 below it).  A
+    perfectly agreeing SSM then commits 9 tokens per verify, as with a budget
+    of 23; a budget of 19 cuts the last leaf."""
+    ps = prompts(4, V, lo=5, hi=9, seed=21)
+    st = {}
+    for budget in (19, 20, 23):
+        res, st[budget] = run_spec(ps, 120, tree_tokens=budget, disagree=0)
+        for p, r in zip(ps, res):
+            assert r.output_tokens == expected(p, 120, V), budget
+    # 20 places exactly what 23 does (no tree is cut), 19 cuts one leaf per
+    # full tree
+    assert st[20].tree_tokens_verified == st[23].tree_tokens_verified
+    assert st[20].llm_steps == st[23].llm_steps
+    assert st[19].tree_tokens_verified < st[20].tree_tokens_verified
+
+
+def test_spec_infer_ssm_capacity_checked_up_front():
+    """An SSM sized by max_tokens_per_batch alone (64) can be handed an init
+    batch of max_requests x 9 verified tokens (8 x 9 = 72) once acceptance is
+    high.  serve_spec_infer checks every SSM's capacity against the largest
+    batch the scheduler can build before the first step, with a message,
+    instead of failing partway through a serve; a model of that size runs."""
+    ps = prompts(8, V, lo=5, hi=9, seed=2)
+    rm = fa.RequestManager(max_requests_per_batch=8, max_tokens_per_batch=64,
+                           max_sequence_length=128, spec_tree_width=(1, 1, 3))
+    llm = fa.HashModel(V, "tree", max_requests=8, max_seq_len=128)
+    rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=8, max_seq_len=128,
+                                       max_tokens=64))
+    with pytest.raises(fa.ffmi.FFMIError, match="holds 64 tokens per step"):
+        fa.generate(rm, llm, ps, max_length=100)
+    rm = fa.RequestManager(max_requests_per_batch=8, max_tokens_per_batch=64,
+                           max_sequence_length=128, spec_tree_width=(1, 1, 3))
+    rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=8, max_seq_len=128,
+                                       max_tokens=72))
+    res = fa.generate(rm, llm, ps, max_length=100)
+    for p, r in zip(ps, res):
+        assert r.output_tokens == expected(p, 100, V)
+
+
+def test_requests_registered_before_the_last_ssm():
+    """Requests registered while fewer SSMs were registered get one beam tree
+    per SSM when the serve starts (each SSM writes its own)."""
+    ps = prompts(3, V, seed=4)
+    rm = fa.RequestManager(max_requests_per_batch=4, max_tokens_per_batch=64,
+                           max_sequence_length=128, spec_tree_width=(1, 1, 3),
+                           spec_extensions=MULTI)
+    llm = fa.HashModel(V, "tree", max_requests=4, max_seq_len=128)
+    rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=4, max_seq_len=128, salt=1))
+    guids = [rm.register_new_request(p, max_length=80) for p in ps]
+    rm.register_ssm_model(fa.HashModel(V, "beam", max_requests=4, max_seq_len=128, salt=2,
+                                       disagree_pct=50))
+    rm.serve_spec_infer(llm)
+    for p, g in zip(ps, guids):
+        assert rm.get_generation_result(g).output_tokens == expected(p, 80, V)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_chained_ssm_steps_equal_stepwise(seed, monkeypatch):
+    """Chained beam steps (the speculation phase's 8 steps staged from
+    placeholder results and launched back to back, the bookkeeping replayed
+    on the results; the hash model runs them as the GPU model does) against
+    the stepwise loop (FFMI_SSM_CHAIN=0): identical tokens, LLM and SSM step
+    counts, tree tokens verified and commits, for random batches, widths,
+    SSM counts and queueing.  Phases where a loading prompt shares a step
+    with running requests of another width run stepwise (the reference's
+    ArgTopK k rule makes the scheduler read past such a step's results)."""
+    rng = np.random.default_rng(9000 + OFF + seed)
+    widths = WIDTHS[int(rng.integers(0, len(WIDTHS)))]
+    nssm = int(rng.integers(1, 4))
+    kw = dict(batch=int(rng.integers(1, 6)), max_tokens=int(rng.integers(24, 96)),
+              widths=widths, tree_tokens=int(rng.choice([23, 40, 64])),
+              ssms=[(int(rng.integers(1, 10 ** 6)), int(rng.choice([0, 30, 100])))
+                    for _ in range(nssm)],
+              ext=W4 | MULTI)
+    ps = prompts(int(rng.integers(1, 9)), V, lo=2, hi=30, seed=seed)
+    ml = int(rng.integers(40, 110))
+    monkeypatch.setenv("FFMI_SSM_CHAIN", "0")
+    ref, st0 = run_spec(ps, ml, **kw)
+    monkeypatch.setenv("FFMI_SSM_CHAIN", "1")
+    res, st1 = run_spec(ps, ml, **kw)
+    assert [r.output_tokens for r in res] == [r.output_tokens for r in ref]
+    assert [r.output_tokens for r in res] == [expected(p, ml, V) for p in ps]
+    for f in ("llm_steps", "ssm_steps", "tokens_committed", "tree_tokens_verified",
+              "request_verifies"):
+        assert getattr(st1, f) == getattr(st0, f), f
+    assert st0.ssm_phases_chained == 0
+    assert st1.ssm_phases_chained > 0
+
+
 def test_spec_infer_ignores_eos_like_the_reference():
     """SpecInfer completes a request on max_length only: the verify path never
     checks EOS (request_manager.cc:1251-1253), unlike incremental decoding
