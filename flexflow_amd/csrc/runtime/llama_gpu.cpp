@@ -115,6 +115,8 @@ struct LlamaGPU : public ffmi_model {
   size_t slot_results[kChain] = {};  // [T][k] ids of each slot
   std::vector<int> slot_map[kChain];  // scheduler entry -> [T][k] index (beam_result_layout)
   hipEvent_t slot_ev[kChain] = {};     // recorded behind each launched slot
+  hipEvent_t chain_t0 = nullptr;       // (FFMI_STEP_TIMING: before a chain's slot 0)
+  bool slot_ev_live[kChain] = {};      // slot_ev recorded for the chain in flight
   int last_slot = -1;                  // highest slot launched since the last wait
   bool chain_ok = !getenv("FFMI_SSM_CHAIN") || atoi(getenv("FFMI_SSM_CHAIN")) != 0;
   size_t slot_ints() const { return (size_t)((o.max_tokens + 15) & ~15) * 4 * 2; }
@@ -312,10 +314,72 @@ struct LlamaGPU : public ffmi_model {
     return T;
   }
 
+  // FFMI_FAULT_TP_AR_DROP: this rank's contribution to one all-reduce zeroed
+  int ar_drop_layer = -1, ar_drop_which = 0;
+  bool ar_drop_now = false;  // (set around the faulted call in enqueue)
+  std::vector<int> head_swapped;  // layers whose Q heads 0 / 1 are exchanged
+
+  // pack the Q rows of layer l with local heads 0 and 1 exchanged (swap) or
+  // in their places; the source rows are regenerated / reloaded
+  ffmi_status pack_q_heads(int l, bool swap) {
+    const int H = c.hidden, s = o.tp_rank;
+    uint16_t *tmp = nullptr;
+    FFMI_HIP(hipMalloc((void **)&tmp, (size_t)H * H * 2));
+    const std::string p = "model.layers." + std::to_string(l) + ".self_attn.q_proj.weight";
+    ffmi_status st = FFMI_OK;
+    if (!weights_folder.empty()) {
+      st = load_tensor(tmp, (size_t)H * H, p);
+    } else if (launch_fill_weight(tmp, (size_t)H * H, ffmi::weight_key(p.c_str(), o.weight_seed),
+                                  0, stream) != hipSuccess) {
+      st = FFMI_ERR_HIP;
+    }
+    if (st == FFMI_OK) {
+      const int pitch = 3 * (Hl / 16);
+      const hipError_t e0 = launch_pack_weight(tmp, H, s * Hl + (swap ? d : 0), 0, d, H,
+                                               layers[l].wqkv, 1, 0, pitch, stream);
+      const hipError_t e1 = launch_pack_weight(tmp, H, s * Hl + (swap ? 0 : d), 0, d, H,
+                                               layers[l].wqkv, 1, d / 16, pitch, stream);
+      if (e0 != hipSuccess || e1 != hipSuccess || hipStreamSynchronize(stream) != hipSuccess)
+        st = FFMI_ERR_HIP;
+    }
+    (void)hipFree(tmp);
+    return st;
+  }
+
   ffmi_status debug_fault(int kind, int layer, int arg) override {
     // the tables are rewritten with blocking copies: finish the model's
     // (non-blocking) stream first in every branch
     if (stream) FFMI_HIP(hipStreamSynchronize(stream));
+    if (kind == FFMI_FAULT_TP_HEAD_SWAP) {
+      FFMI_CHECK(layer >= -1 && layer < c.num_layers && heads_l >= 2 && d % 16 == 0,
+                 FFMI_ERR_INVALID);
+      for (int l = 0; l < c.num_layers; ++l)
+        if ((layer < 0 || l == layer) &&
+            std::find(head_swapped.begin(), head_swapped.end(), l) == head_swapped.end()) {
+          ffmi_status st = pack_q_heads(l, true);
+          if (st != FFMI_OK) return st;
+          head_swapped.push_back(l);
+        }
+      clear_graphs();
+      return FFMI_OK;
+    }
+    if (kind == FFMI_FAULT_TP_AR_DROP) {
+      FFMI_CHECK(o.tp_size > 1 && layer >= 0 && layer < c.num_layers && (arg == 0 || arg == 1),
+                 FFMI_ERR_INVALID);
+      ar_drop_layer = layer;
+      ar_drop_which = arg;
+      clear_graphs();
+      return FFMI_OK;
+    }
+    if (kind == FFMI_FAULT_NONE) {
+      for (int l : head_swapped) {
+        ffmi_status st = pack_q_heads(l, false);
+        if (st != FFMI_OK) return st;
+      }
+      head_swapped.clear();
+      ar_drop_layer = -1;
+      clear_graphs();
+    }
     if (kind == FFMI_FAULT_RESID_ROUND || kind == FFMI_FAULT_NONE) {
       // captured graphs hold the launches of the other norm variant
       ffmi::set_norm_fault(kind == FFMI_FAULT_RESID_ROUND);
@@ -341,14 +405,22 @@ struct LlamaGPU : public ffmi_model {
 
   ~LlamaGPU() override {
     if (stream) (void)hipStreamSynchronize(stream);
-    for (auto &kv : st_sum)
+    for (auto &kv : st_sum) {
+      if (kv.first < 0) {
+        fprintf(stderr, "[ffmi step timing] H=%d chain of %d steps: %ld chains, gpu span %.1f us "
+                "(%.1f us per step)\n", c.hidden, -kv.first, kv.second.n,
+                kv.second.gpu / kv.second.n, kv.second.gpu / kv.second.n / -kv.first);
+        continue;
+      }
       fprintf(stderr, "[ffmi step timing] H=%d T=%d steps=%ld launch=%.1f gpu=%.1f wait=%.1f total=%.1f us\n",
               c.hidden, kv.first, kv.second.n, kv.second.launch / kv.second.n, kv.second.gpu / kv.second.n,
               kv.second.wait / kv.second.n, kv.second.total / kv.second.n);
+    }
     for (auto e : st_ev)
       if (e) (void)hipEventDestroy(e);
     for (auto e : slot_ev)
       if (e) (void)hipEventDestroy(e);
+    if (chain_t0) (void)hipEventDestroy(chain_t0);
     clear_graphs();
     for (auto &L : layers) ffmi_attn_destroy(L.attn);
     for (auto e : ev_pool) (void)hipEventDestroy(e);
@@ -650,11 +722,14 @@ struct LlamaGPU : public ffmi_model {
   ffmi_status rowpar_gemm_allreduce(const uint16_t *X, const uint16_t *W, int K, uint16_t *out,
                                     int T, int XP) {
     const int H = c.hidden;
+    // (FFMI_FAULT_TP_AR_DROP: the GEMM's output zeroed before the all-reduce)
+    const bool drop = ar_drop_now;
     if (!(peer || rccl) || tp_chunks == 1) {
       // over the transport the split-K reduce is the all-reduce's copy-in
       ffmi::Partials part;
       FFMI_HIP(ffmi::launch_gemm(X, W, out, ws, ws_bytes, T, H, K, XP, stream,
-                                 peer && ar_slabs ? &part : nullptr));
+                                 peer && ar_slabs && !drop ? &part : nullptr));
+      if (drop) FFMI_HIP(hipMemsetAsync(out, 0, (size_t)T * H * 2, stream));
       if (peer)
         return ffmi::comm_allreduce_cols(o.comm, out, out, T, H, H, 0, FFMI_F16, stream,
                                          part.S > 0 ? &part : nullptr);
@@ -668,11 +743,12 @@ struct LlamaGPU : public ffmi_model {
       // over the transport: the chunk's split-K slabs (own workspace region)
       // go to the all-reduce's copy-in, no reduce pass on this stream
       ffmi::Partials part;
-      const bool def = peer && ar_slabs;
+      const bool def = peer && ar_slabs && !drop;
       FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb,
                                  def ? (float *)((char *)ws + ch * ws_chunk) : ws,
                                  def ? ws_chunk : ws_bytes, T, Hc, K, XP, stream,
                                  def ? &part : nullptr, H / 16));
+      if (drop) FFMI_HIP(hipMemsetAsync(cb, 0, (size_t)T * Hc * 2, stream));
       FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
       FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
       if (peer) {  // the transport reduces straight into out's columns
@@ -950,7 +1026,9 @@ struct LlamaGPU : public ffmi_model {
         mk();
       } else {  // GEMM + all-reduce (overlapped over xGMI): timed together
         pr = prof_begin(on);
+        ar_drop_now = l == ar_drop_layer && ar_drop_which == 0;
         TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
+        ar_drop_now = false;
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
         mk();
       }
@@ -989,7 +1067,9 @@ struct LlamaGPU : public ffmi_model {
         mk();  // (two back to back: the marker-to-marker boundary itself)
       } else {
         pr = prof_begin(on);
+        ar_drop_now = l == ar_drop_layer && ar_drop_which == 1;
         TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
+        ar_drop_now = false;
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
         mk();
       }
@@ -1112,6 +1192,10 @@ struct LlamaGPU : public ffmi_model {
         ti.token_id = -1 - slot_map[slot - 1][i];
       }
     const int k = ps.topk;
+    if (step_timing && slot == 0) {
+      if (!chain_t0) FFMI_HIP(hipEventCreate(&chain_t0));
+      FFMI_HIP(hipEventRecord(chain_t0, stream));
+    }
     cur_slot = slot;
     batch = chain_batch[slot];
     slot_results[slot] = (size_t)bc.num_tokens * k;
@@ -1119,22 +1203,42 @@ struct LlamaGPU : public ffmi_model {
     ffmi_status st = forward_launch(k);
     batch = chain_batch[0];
     cur_slot = 0;
-    if (st == FFMI_OK) {
+    // per-slot events let the scheduler replay slot d while later slots run,
+    // but each costs the GPU more than the replay it overlaps (same-box A/B,
+    // tokens/s: 1342 without, 1333 with, 1326 stepwise): off unless
+    // FFMI_CHAIN_EVENTS=1; the collect then waits for the whole chain
+    static const bool slot_events = getenv("FFMI_CHAIN_EVENTS") && atoi(getenv("FFMI_CHAIN_EVENTS"));
+    if (st == FFMI_OK && !slot_events) last_slot = slot;
+    if (st == FFMI_OK && slot_events) {
       // (so that the scheduler can collect this slot while later ones run)
-      if (!slot_ev[slot]) FFMI_HIP(hipEventCreateWithFlags(&slot_ev[slot], hipEventDisableTiming));
+      if (!slot_ev[slot])
+        FFMI_HIP(hipEventCreateWithFlags(&slot_ev[slot], step_timing ? 0 : hipEventDisableTiming));
       FFMI_HIP(hipEventRecord(slot_ev[slot], stream));
+      slot_ev_live[slot] = true;
       last_slot = slot;
     }
     return st;
   }
   ffmi_status beam_collect_chained(int slot, BeamInferenceResult *ir) override {
     FFMI_CHECK(slot >= 0 && slot < kChain, FFMI_ERR_INVALID);
-    if (slot < last_slot && slot_ev[slot]) {
+    if (slot < last_slot && slot_ev[slot] && slot_ev_live[slot]) {
       // later slots still run: wait for this one only
       FFMI_HIP(hipEventSynchronize(slot_ev[slot]));
     } else {
+      const int ls = last_slot;
       ffmi_status st = forward_finish();  // (every launched step: one stream)
       if (st != FFMI_OK) return st;
+      for (bool &b : slot_ev_live) b = false;
+      // FFMI_STEP_TIMING: the GPU span of a whole chain, from the event before
+      // slot 0's launch to the one after the last slot
+      if (step_timing && ls > 0 && chain_t0) {
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, chain_t0, slot_ev[ls]) == hipSuccess) {
+          StepTime &q = st_sum[-(ls + 1)];
+          q.n++;
+          q.gpu += ms * 1e3;
+        }
+      }
       last_slot = -1;
     }
     const size_t n = slot_results[slot];

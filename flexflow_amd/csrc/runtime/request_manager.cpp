@@ -1170,6 +1170,7 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   };
   bool chainable = st == FFMI_OK;
   const double tp0 = now_us();
+  chain_t[0] += tp0 - ts;
   for (size_t s = 0; s < n && chainable; ++s) {
     spec[s * D] = (*beam_vec)[s];
     for (int d = 1; d < D && chainable; ++d) {
@@ -1192,14 +1193,18 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
     if (it != saved_steps.end()) kv.second.ssm_decoding_steps = it->second;
   }
   prep_us += now_us() - tp0;
+  chain_t[1] += now_us() - tp0;
   // launch steps 1 .. D-1 back to back (chainable), or nothing more yet
   if (chainable) stats.ssm_phases_chained++;
   size_t launched = launched0;
+  const double tl0 = now_us();
   for (int d = 1; d < D && chainable && st == FFMI_OK; ++d)
     for (size_t s = 0; s < n && st == FFMI_OK; ++s) {
       st = ssm_models[s]->beam_launch_chained(spec[s * D + d], d);
       if (st == FFMI_OK) ++launched;
     }
+  chain_t[2] += now_us() - tl0;
+  chain_t[4] += 1;
   // collect in the stepwise loop's order, replaying the bookkeeping on the
   // real results; unchained: collect, prepare, launch the next step (slot 0)
   for (int d = 0; d < D; ++d)
@@ -1230,6 +1235,7 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   // host scheduling, as in the stepwise loop
   (void)prep_us;
   stats.ssm_us += t_last - ts;
+  chain_t[3] += t_last - ts;
   return st;
 }
 
@@ -1375,6 +1381,11 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   delete beam_ir;
   delete beam_vec;
   stats.wall_us = now_us() - t0;
+  if (getenv("FFMI_STEP_TIMING") && chain_t[4] > 0)
+    fprintf(stderr, "[ffmi chain timing] %.0f phases: launch step 0 %.1f us, stage steps 1-7 %.1f us, "
+            "launch steps 1-7 %.1f us, phase to last result %.1f us\n", chain_t[4],
+            chain_t[0] / chain_t[4], chain_t[1] / chain_t[4], chain_t[2] / chain_t[4],
+            chain_t[3] / chain_t[4]);
   return st;
 }
 

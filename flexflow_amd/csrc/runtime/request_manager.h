@@ -200,6 +200,7 @@ class RequestManager {
   size_t num_processed_requests = 0;
   std::vector<BeamSearchBatchConfig> chain_spec;  // staged chained beam batches
   std::unique_ptr<BeamInferenceResult> chain_ph;   // placeholder results (-1 - i)
+  double chain_t[5] = {};  // (FFMI_STEP_TIMING: host-side phase timings, count)
 };
 
 double now_us();

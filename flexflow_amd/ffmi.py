@@ -32,7 +32,7 @@ W_STREAM = 0x40  # FFMI_W_STREAM: non-temporal weight loads (speed only)
 F16, F32, I32 = 0, 1, 2
 # synthetic weight inits (ffmi_model_opts.weight_init) and fault kinds
 WEIGHT_INITS = {"uniform": 0, "depth_scaled": 1, "token_chain": 2}
-FAULT_NONE, FAULT_ROPE_POS, FAULT_RESID_ROUND = 0, 1, 2
+FAULT_NONE, FAULT_ROPE_POS, FAULT_RESID_ROUND, FAULT_TP_HEAD_SWAP, FAULT_TP_AR_DROP = 0, 1, 2, 3, 4
 # flagged SpecInfer extensions (include/ffmi.h FFMI_SPEC_EXT_*)
 SPEC_EXT_WIDTH4, SPEC_EXT_MULTI_SSM = 1, 2
 ATTN_QTILE = 32

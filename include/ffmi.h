@@ -445,10 +445,19 @@ long ffmi_model_debug_width(ffmi_model *m, int which);
  *     x1 + x2 where residual_rms_norm_kernels.cu:112-114 rounds it to half
  *     first -- a rounding-point bug that moves the normalised outputs by at
  *     most an ulp (the norms folded into the decode GEMMs are not faulted).
+ *   FFMI_FAULT_TP_HEAD_SWAP (layer; -1: every layer; fp16 models): this
+ *     model's qkv weights with the Q rows of its local heads 0 and 1
+ *     exchanged -- a head-offset bug in one rank's shard (file_loader.cc:
+ *     286-303 places head h's rows at h * head_dim of the rank's block).
+ *   FFMI_FAULT_TP_AR_DROP (layer, arg: 0 = the all-reduce after o_proj, 1 =
+ *     after down_proj; TP > 1, fp16 models): this rank's contribution to that
+ *     all-reduce is zeroed (a partial sum lost, allreduce.cc:291-331).
  *   FFMI_FAULT_NONE clears every fault. */
 #define FFMI_FAULT_NONE 0
 #define FFMI_FAULT_ROPE_POS 1
 #define FFMI_FAULT_RESID_ROUND 2
+#define FFMI_FAULT_TP_HEAD_SWAP 3
+#define FFMI_FAULT_TP_AR_DROP 4
 ffmi_status ffmi_model_debug_fault(ffmi_model *m, int kind, int layer, int arg);
 /* select the HIP device of the calling thread (one process per GPU) */
 ffmi_status ffmi_set_device(int device);

@@ -110,3 +110,26 @@ def expected_flips(z0, z1):
     gap = top[:, 1] - top[:, 0]
     x = -gap / np.maximum(sig, 1e-30)
     return float(sum(0.5 * math.erfc(-v / math.sqrt(2.0)) for v in x))
+
+
+def expected_flips_all(z0, z1, competitors=16):
+    """expected_flips with every competitor, not the runner-up alone: for
+    each row the union bound sum_j Phi(-(z0[top] - z0[j]) / sigma_pair) over
+    the `competitors` next-largest logits (a third candidate within the noise
+    flips a pick as well as the second; the round-5 TP test met 26 ties
+    against 13.6 from the top-2 formula).  An upper estimate of the expected
+    flip count, fixed before the data: the tie budget is then
+    budget_from_expected(E), a Poisson 3-sigma bound."""
+    z0 = np.asarray(z0, np.float64)
+    d = np.asarray(z1, np.float64) - z0
+    sig = np.maximum(np.sqrt(2.0) * d.std(axis=1), 1e-30)
+    srt = -np.sort(-z0, axis=1)[:, :competitors + 1]
+    gaps = srt[:, :1] - srt[:, 1:]
+    x = gaps / sig[:, None]
+    return float(0.5 * np.sum([math.erfc(v / math.sqrt(2.0)) for v in x.ravel()]))
+
+
+def budget_from_expected(e):
+    """ties allowed when e flips are expected: e + 3 sqrt(e) + 2"""
+    return int(math.ceil(e + 3.0 * math.sqrt(e) + 2.0))
+

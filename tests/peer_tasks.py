@@ -111,13 +111,18 @@ def vshard_task(fa, comm, rank, n, T, V, k, seed):
 
 
 def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ssm_cfg,
-                     tf_seqs=(), weight_init=0):
+                     tf_seqs=(), weight_init=0, fault=None):
     """One TP shard per rank of a full-depth model over the xGMI transport:
     incr decoding (spec False) or SpecInfer with the SSM replicated on every
     rank (spec_infer.cc:385-387).  Then, in incr mode, a teacher-forced pass:
     the sequences `tf_seqs` (+ this run's own) as ONE prefill step with the
     logits captured (this rank's vocab shard, [T][V/n]); the row predicting
     token j + 1 of sequence s is s's j-th row of its block."""
+    # fault = (kind, layer, arg, rank): a negative control on that rank's
+    # shard only (ffmi_model_debug_fault FFMI_FAULT_TP_*)
+    def apply_fault(m):
+        if fault is not None and rank == fault[3]:
+            m.debug_fault(fault[0], fault[1], fault[2])
     B = len(prompts)
     mtb = 256
     if spec:  # True or a tests/spec_configs.py name; the SSMs replicated per rank
@@ -127,6 +132,7 @@ def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ss
         m = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
                      max_tree_tokens=tt, weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm,
                      weight_init=weight_init)
+        apply_fault(m)
         res = fa.generate(rm, m, prompts, max_length=max_length, spec=True)
         out = {"tokens": [r.output_tokens for r in res], "llm_steps": rm.stats().llm_steps}
         m.close()
@@ -136,6 +142,7 @@ def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ss
     nt = B + len(tf_seqs)
     m = fa.Model(cfg, "inc", max_requests=max(B, nt), max_tokens=2 * mtb, max_seq_len=128,
                  weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm, weight_init=weight_init)
+    apply_fault(m)
     rm = fa.RequestManager(max_requests_per_batch=max(B, nt), max_tokens_per_batch=mtb,
                            max_sequence_length=128)
     res = fa.generate(rm, m, prompts, max_length=max_length)
