@@ -716,6 +716,10 @@ struct ffmi_comm {
   int nranks = 1, rank = 0;
   std::shared_ptr<LocalGroup> local;
   std::unique_ptr<PeerState> peer;
+  // ffmi_comm_allgather: device scratch and stream (created on first use)
+  float *xg = nullptr;
+  size_t xg_cap = 0;
+  hipStream_t xg_stream = nullptr;
 };
 
 extern "C" ffmi_status ffmi_comm_create_local(int nranks, ffmi_comm **out) {
@@ -796,8 +800,60 @@ extern "C" ffmi_status ffmi_comm_create(const void *id, int nranks, int rank, ff
 
 extern "C" void ffmi_comm_destroy(ffmi_comm *c) {
   if (!c) return;
+  if (c->xg_stream) (void)hipStreamSynchronize(c->xg_stream);
+  if (c->xg) (void)hipFree(c->xg);
+  if (c->xg_stream) (void)hipStreamDestroy(c->xg_stream);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
+}
+
+// All-gather of host byte blocks as an fp32 sum all-reduce that every
+// transport carries: each 16-bit half-word becomes an exact small integer in
+// a float, a rank fills its own slot and zeroes the others, and x + 0 = x
+// (no rounding, no -0 / denormal / NaN bit patterns in flight).
+extern "C" ffmi_status ffmi_comm_allgather(ffmi_comm *c, const void *mine, size_t bytes,
+                                           void *all) {
+  FFMI_CHECK(c && (mine || !bytes) && (all || !bytes), FFMI_ERR_INVALID);
+  const int n = c->nranks;
+  if (n == 1) {
+    if (bytes) memcpy(all, mine, bytes);
+    return FFMI_OK;
+  }
+  const size_t words = (bytes + 1) / 2;  // 16-bit words per rank
+  const size_t count = words * n;
+  if (c->xg_cap < count) {
+    if (c->xg) FFMI_HIP(hipFree(c->xg));
+    c->xg = nullptr;
+    c->xg_cap = 0;
+    FFMI_HIP(hipMalloc((void **)&c->xg, count * sizeof(float)));
+    c->xg_cap = count;
+  }
+  if (!c->xg_stream) FFMI_HIP(hipStreamCreateWithFlags(&c->xg_stream, hipStreamNonBlocking));
+  std::vector<float> h(count, 0.0f);
+  std::vector<uint16_t> w(words, 0);
+  memcpy(w.data(), mine, bytes);
+  for (size_t i = 0; i < words; ++i) h[(size_t)c->rank * words + i] = (float)w[i];
+  FFMI_HIP(hipMemcpyAsync(c->xg, h.data(), count * sizeof(float), hipMemcpyHostToDevice,
+                          c->xg_stream));
+  ffmi_status st = ffmi_allreduce(c, c->xg, c->xg, count, FFMI_F32, (ffmi_stream)c->xg_stream);
+  if (st != FFMI_OK) return st;
+  FFMI_HIP(hipMemcpyAsync(h.data(), c->xg, count * sizeof(float), hipMemcpyDeviceToHost,
+                          c->xg_stream));
+  FFMI_HIP(hipStreamSynchronize(c->xg_stream));
+  if (c->peer && c->peer->attached) {
+    st = ffmi_comm_peer_status(c);
+    if (st != FFMI_OK) return st;
+  }
+  std::vector<uint16_t> out(words);
+  for (int r = 0; r < n; ++r) {
+    for (size_t i = 0; i < words; ++i) {
+      const float v = h[(size_t)r * words + i];
+      if (!(v >= 0.0f && v <= 65535.0f && v == (float)(uint16_t)v)) return FFMI_ERR_NCCL;
+      out[i] = (uint16_t)v;
+    }
+    memcpy(static_cast<char *>(all) + (size_t)r * bytes, out.data(), bytes);
+  }
+  return FFMI_OK;
 }
 
 extern "C" ffmi_status ffmi_comm_create_peer(int nranks, int rank, ffmi_comm **out) {
@@ -962,6 +1018,7 @@ bool comm_has_peer(const ffmi_comm *c, size_t bytes) {
   return c && c->peer && c->peer->attached && bytes <= c->peer->cap;
 }
 int comm_size(const ffmi_comm *c) { return c ? c->nranks : 1; }
+int comm_rank(const ffmi_comm *c) { return c ? c->rank : 0; }
 bool comm_peer_attached(const ffmi_comm *c) { return c && c->peer && c->peer->attached; }
 bool comm_has_fallback(const ffmi_comm *c) { return c && (c->comm || c->local); }
 bool comm_is_rccl(const ffmi_comm *c) { return c && c->comm && !c->local; }

@@ -284,6 +284,7 @@ ffmi_status batch_copy(ffmi_batch_dev *b, size_t bytes, hipStream_t s, bool reco
 // transport when attached and the message fits its buffers.
 bool comm_has_peer(const ffmi_comm *c, size_t bytes);
 int comm_size(const ffmi_comm *c);
+int comm_rank(const ffmi_comm *c);
 // the xGMI transport is attached (whatever its capacity)
 bool comm_peer_attached(const ffmi_comm *c);
 // an RCCL communicator or an in-process group takes what the transport cannot

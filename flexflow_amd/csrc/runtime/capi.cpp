@@ -111,6 +111,30 @@ extern "C" ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm) {
   return FFMI_OK;
 }
 
+extern "C" ffmi_status ffmi_rm_register_remote_ssm(ffmi_rm *rm) {
+  if (!rm) return FFMI_ERR_INVALID;
+  rm->rm.register_ssm_model(nullptr);
+  return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_rm_set_ssm_exchange(ffmi_rm *rm, int nranks, int rank,
+                                                ffmi_allgather_fn fn, void *ctx) {
+  if (!rm || nranks < 1 || rank < 0 || rank >= nranks || (nranks > 1 && !fn))
+    return FFMI_ERR_INVALID;
+  rm->rm.set_ssm_exchange(nranks, rank, fn, ctx);
+  return FFMI_OK;
+}
+
+static int comm_allgather_cb(void *ctx, const void *mine, size_t bytes, void *all) {
+  return ffmi_comm_allgather(static_cast<ffmi_comm *>(ctx), mine, bytes, all) == FFMI_OK ? 0 : 1;
+}
+
+extern "C" ffmi_status ffmi_rm_set_ssm_exchange_comm(ffmi_rm *rm, ffmi_comm *comm) {
+  if (!rm || !comm) return FFMI_ERR_INVALID;
+  rm->rm.set_ssm_exchange(ffmi::comm_size(comm), ffmi::comm_rank(comm), comm_allgather_cb, comm);
+  return FFMI_OK;
+}
+
 extern "C" ffmi_status ffmi_rm_register_output_filepath(ffmi_rm *rm, const char *path) {
   if (!rm) return FFMI_ERR_INVALID;
   rm->rm.register_output_filepath(path ? path : "");
@@ -184,5 +208,6 @@ extern "C" ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s) {
   s->ssm_us = rm->rm.stats.ssm_us;
   s->wall_us = rm->rm.stats.wall_us;
   s->ssm_phases_chained = rm->rm.stats.ssm_phases_chained;
+  s->ssm_exchange_us = rm->rm.stats.ssm_exchange_us;
   return FFMI_OK;
 }

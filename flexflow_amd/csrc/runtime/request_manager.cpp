@@ -1127,15 +1127,16 @@ static bool same_beam_batch(const BeamSearchBatchConfig &spec, const BeamSearchB
 // never a silent divergence).
 ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchConfig> *beam_vec,
                                                   BeamInferenceResult *beam_ir) {
-  const size_t n = ssm_models.size();
+  const std::vector<int> &loc = ssm_local;  // (the SSMs this rank runs)
+  const size_t n = loc.size();
   const int D = BeamSearchBatchConfig::MAX_BEAM_DEPTH;
   const double ts = now_us();
   double prep_us = 0, t_last = ts;
   ffmi_status st = FFMI_OK;
   // step 0 of every SSM (its tokens are known)
   size_t launched0 = 0;
-  for (size_t s = 0; s < n && st == FFMI_OK; ++s) {
-    st = ssm_models[s]->beam_launch_chained((*beam_vec)[s], 0);
+  for (size_t i = 0; i < n && st == FFMI_OK; ++i) {
+    st = ssm_models[loc[i]]->beam_launch_chained((*beam_vec)[loc[i]], 0);
     if (st == FFMI_OK) ++launched0;
   }
   // the state prepare_next_batch_beam writes, saved for the replay
@@ -1171,12 +1172,12 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   bool chainable = st == FFMI_OK;
   const double tp0 = now_us();
   chain_t[0] += tp0 - ts;
-  for (size_t s = 0; s < n && chainable; ++s) {
-    spec[s * D] = (*beam_vec)[s];
+  for (size_t i = 0; i < n && chainable; ++i) {
+    spec[i * D] = (*beam_vec)[loc[i]];
     for (int d = 1; d < D && chainable; ++d) {
-      spec[s * D + d] = prepare_next_batch_beam(spec[s * D + d - 1], *chain_ph);
-      const long have = results_of(spec[s * D + d - 1]);
-      const BeamSearchBatchConfig &b = spec[s * D + d];
+      spec[i * D + d] = prepare_next_batch_beam(spec[i * D + d - 1], *chain_ph);
+      const long have = results_of(spec[i * D + d - 1]);
+      const BeamSearchBatchConfig &b = spec[i * D + d];
       for (int t = 0; t < b.num_tokens; ++t)
         if (b.tokensInfo[t].token_id < 0 && -1L - b.tokensInfo[t].token_id >= have)
           chainable = false;
@@ -1199,8 +1200,8 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   size_t launched = launched0;
   const double tl0 = now_us();
   for (int d = 1; d < D && chainable && st == FFMI_OK; ++d)
-    for (size_t s = 0; s < n && st == FFMI_OK; ++s) {
-      st = ssm_models[s]->beam_launch_chained(spec[s * D + d], d);
+    for (size_t i = 0; i < n && st == FFMI_OK; ++i) {
+      st = ssm_models[loc[i]]->beam_launch_chained(spec[i * D + d], d);
       if (st == FFMI_OK) ++launched;
     }
   chain_t[2] += now_us() - tl0;
@@ -1208,9 +1209,10 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   // collect in the stepwise loop's order, replaying the bookkeeping on the
   // real results; unchained: collect, prepare, launch the next step (slot 0)
   for (int d = 0; d < D; ++d)
-    for (size_t s = 0; s < n; ++s) {
-      const bool was_launched = chainable ? (size_t)d * n + s < launched
-                                          : (d == 0 ? s < launched0 : st == FFMI_OK);
+    for (size_t i = 0; i < n; ++i) {
+      const int s = loc[i];
+      const bool was_launched = chainable ? (size_t)d * n + i < launched
+                                          : (d == 0 ? i < launched0 : st == FFMI_OK);
       if (!was_launched) continue;
       const ffmi_status cs = ssm_models[s]->beam_collect_chained(chainable ? d : 0, beam_ir);
       t_last = now_us();
@@ -1218,9 +1220,10 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
       if (st != FFMI_OK) continue;  // (collect the rest: nothing left in flight)
       stats.ssm_steps++;
       const double tp = now_us();
+      record_step(s, d, (*beam_vec)[s], *beam_ir);
       (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
       if (chainable && d + 1 < D &&
-          !same_beam_batch(spec[s * D + d + 1], (*beam_vec)[s], *beam_ir, max_requests_per_batch)) {
+          !same_beam_batch(spec[i * D + d + 1], (*beam_vec)[s], *beam_ir, max_requests_per_batch)) {
         ffmi_set_last_error("chained SSM beam steps: a staged batch differs from the one its "
                             "results give (FFMI_SSM_CHAIN=0 runs the steps one by one)",
                             __FILE__, __LINE__);
@@ -1239,6 +1242,99 @@ ffmi_status RequestManager::run_ssm_phase_chained(std::vector<BeamSearchBatchCon
   return st;
 }
 
+// Distributed SSMs (set_ssm_exchange).  A local SSM's results of each step,
+// in the scheduler's layout (beam_result_layout: what store_beam_metadata
+// reads), are kept for the exchange.
+void RequestManager::record_step(int s, int depth, const BeamSearchBatchConfig &bc,
+                                 const BeamInferenceResult &ir) {
+  if (xch_world <= 1) return;
+  std::vector<int> layout;
+  beam_result_layout(bc, &layout);
+  StepRecord &r = phase_rec.at(s).at(depth);
+  r.ids.assign(ir.token_ids, ir.token_ids + layout.size());
+  r.probs.assign(ir.probs, ir.probs + layout.size());
+}
+
+// After the local SSMs' speculation phase: every rank's records, then each
+// remote SSM's MAX_BEAM_DEPTH prepare_next_batch_beam calls replayed on its
+// results from the same init batch.  prepare_next_batch_beam of SSM s writes
+// only SSM s's beam trees, plus counters that commute (ssm_decoding_steps) or
+// belong to SSM 0 alone (ssm_cache_size), so the order of SSMs does not
+// matter: every rank ends with the trees, counters and batches of a run with
+// every SSM local.  Records are int32 words: [k SSMs] then per SSM [s, then
+// per depth n_d, n_d ids, n_d probs (float bits)]; one all-gather of the
+// sizes, one of the records padded to the largest.
+ffmi_status RequestManager::exchange_and_replay(std::vector<BeamSearchBatchConfig> *beam_vec,
+                                                BeamInferenceResult *beam_ir) {
+  const int D = BeamSearchBatchConfig::MAX_BEAM_DEPTH;
+  const int W = xch_world;
+  std::vector<int32_t> mine;
+  mine.push_back((int32_t)ssm_local.size());
+  for (int s : ssm_local) {
+    mine.push_back(s);
+    for (int d = 0; d < D; ++d) {
+      const StepRecord &r = phase_rec[s][d];
+      mine.push_back((int32_t)r.ids.size());
+      mine.insert(mine.end(), r.ids.begin(), r.ids.end());
+      for (float p : r.probs) {
+        int32_t b;
+        memcpy(&b, &p, 4);
+        mine.push_back(b);
+      }
+    }
+  }
+  int64_t len = (int64_t)mine.size();
+  std::vector<int64_t> lens(W, 0);
+  if (xch_fn(xch_ctx, &len, sizeof len, lens.data()) != 0) {
+    ffmi_set_last_error("SSM exchange (sizes) failed", __FILE__, __LINE__);
+    return FFMI_ERR_NCCL;
+  }
+  int64_t mx = 0;
+  for (int64_t l : lens) mx = std::max(mx, l);
+  if (mx <= 0 || mx > (int64_t)1 << 26) return FFMI_ERR_INVALID;
+  mine.resize((size_t)mx, 0);
+  std::vector<int32_t> all((size_t)mx * W);
+  if (xch_fn(xch_ctx, mine.data(), (size_t)mx * 4, all.data()) != 0) {
+    ffmi_set_last_error("SSM exchange (records) failed", __FILE__, __LINE__);
+    return FFMI_ERR_NCCL;
+  }
+  std::vector<bool> have(ssm_models.size(), false);
+  for (int s : ssm_local) have[s] = true;
+  std::vector<int> layout;
+  for (int r = 0; r < W; ++r) {
+    if (r == xch_rank) continue;
+    const int32_t *p = all.data() + (size_t)r * mx;
+    const int32_t *end = p + lens[r];
+    auto take = [&]() -> int32_t { return p < end ? *p++ : INT32_MIN; };
+    const int k = take();
+    for (int j = 0; j < k; ++j) {
+      const int s = take();
+      FFMI_CHECK(s >= 0 && s < (int)ssm_models.size() && !ssm_models[s] && !have[s],
+                 FFMI_ERR_INVALID);
+      have[s] = true;
+      for (int d = 0; d < D; ++d) {
+        const int nd = take();
+        beam_result_layout((*beam_vec)[s], &layout);
+        FFMI_CHECK(nd == (int)layout.size() && end - p >= 2L * nd, FFMI_ERR_INVALID);
+        for (int i = 0; i < nd; ++i) {
+          beam_ir->token_ids[i] = p[i];
+          memcpy(&beam_ir->probs[i], &p[nd + i], 4);
+          beam_ir->parent_id[i] = 0;
+        }
+        p += 2 * nd;
+        (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
+      }
+    }
+  }
+  for (size_t s = 0; s < ssm_models.size(); ++s)
+    if (!have[s]) {
+      ffmi_set_last_error("SSM exchange: no rank ran one of the registered SSMs", __FILE__,
+                          __LINE__);
+      return FFMI_ERR_INVALID;
+    }
+  return FFMI_OK;
+}
+
 // request_manager.cc:3083-3173
 ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   if (!llm) return FFMI_ERR_INVALID;
@@ -1254,19 +1350,34 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   // chunks up to max_tokens_per_batch, a beam step every request's beams
   // (up to MAX_SPECULATIVE_TREE_BRANCHES each) or prompt chunks up to the
   // same budget.  Checked here rather than failing partway through a serve
+  // placement: SSM s runs on rank s % nranks (set_ssm_exchange); without an
+  // exchange every SSM is local
+  ssm_local.clear();
+  for (size_t s = 0; s < ssm_models.size(); ++s) {
+    const bool mine = xch_world <= 1 || (int)(s % xch_world) == xch_rank;
+    if (mine != (ssm_models[s] != nullptr) || (xch_world > 1 && !xch_fn)) {
+      ffmi_set_last_error("SpecInfer: SSM s must be a model on rank s % nranks and a remote "
+                          "placeholder on the other ranks (set_ssm_exchange)", __FILE__, __LINE__);
+      return FFMI_ERR_INVALID;
+    }
+    if (mine) ssm_local.push_back((int)s);
+  }
+  if (xch_world > 1)
+    phase_rec.assign(ssm_models.size(),
+                     std::vector<StepRecord>(BeamSearchBatchConfig::MAX_BEAM_DEPTH));
   {
     const int need = std::max(max_tokens_per_batch,
                               max_requests_per_batch *
                                   std::max(BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1,
                                            (int)BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES));
-    for (size_t s = 0; s < ssm_models.size(); ++s) {
+    for (int s : ssm_local) {
       const int cap = ssm_models[s]->token_capacity();
       if (cap >= 0 && cap < need) {
         char msg[256];
         snprintf(msg, sizeof msg,
                  "SpecInfer: SSM %zu holds %d tokens per step, the scheduler can build %d "
                  "(max(max_tokens_per_batch, max_requests x %d)): create it with max_tokens >= %d",
-                 s, cap, need,
+                 (size_t)s, cap, need,
                  std::max(BeamSearchBatchConfig::MAX_BEAM_DEPTH + 1,
                           (int)BeamSearchBatchConfig::MAX_SPECULATIVE_TREE_BRANCHES),
                  need);
@@ -1284,12 +1395,12 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
   // SSMs whose steps run collectives (TP-sharded) are stepped one at a time:
   // their steps' all-reduces must reach every rank in the same order
   bool overlap_ssms = true;
-  for (auto *m : ssm_models)
-    if (m->uses_collectives()) overlap_ssms = false;
+  for (int s : ssm_local)
+    if (ssm_models[s]->uses_collectives()) overlap_ssms = false;
   // chained beam steps where every SSM supports them (FFMI_SSM_CHAIN=0: off)
   bool chain = overlap_ssms && !(getenv("FFMI_SSM_CHAIN") && atoi(getenv("FFMI_SSM_CHAIN")) == 0);
-  for (auto *m : ssm_models)
-    if (!m->can_chain_beam()) chain = false;
+  for (int s : ssm_local)
+    if (!ssm_models[s]->can_chain_beam()) chain = false;
   apply_limits();
   stats = Stats();
   const double t0 = now_us();
@@ -1323,30 +1434,33 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
     if (chain) {
       st = run_ssm_phase_chained(beam_vec, beam_ir);
     } else {
+      const std::vector<int> &loc = ssm_local;
       const size_t n = ssm_models.size();
       const double ts = now_us();
       double prep_us = 0;
       std::vector<bool> inflight(n, false);
       if (!overlap_ssms) {
         // one step in flight at a time, SSM by SSM (the reference's order)
-        for (size_t s = 0; s < n && st == FFMI_OK; s++)
+        for (size_t i = 0; i < loc.size() && st == FFMI_OK; i++)
           for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && st == FFMI_OK;
                depth++) {
+            const int s = loc[i];
             st = ssm_models[s]->beam_launch((*beam_vec)[s]);
             if (st == FFMI_OK) st = ssm_models[s]->beam_collect(beam_ir);
             if (st != FFMI_OK) break;
             stats.ssm_steps++;
             const double tp = now_us();
+            record_step(s, depth, (*beam_vec)[s], *beam_ir);
             (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
             prep_us += now_us() - tp;
           }
       }
-      for (size_t s = 0; s < n && st == FFMI_OK && overlap_ssms; s++) {
-        st = ssm_models[s]->beam_launch((*beam_vec)[s]);
-        inflight[s] = st == FFMI_OK;
+      for (size_t i = 0; i < loc.size() && st == FFMI_OK && overlap_ssms; i++) {
+        st = ssm_models[loc[i]]->beam_launch((*beam_vec)[loc[i]]);
+        inflight[loc[i]] = st == FFMI_OK;
       }
       for (int depth = 0; depth < BeamSearchBatchConfig::MAX_BEAM_DEPTH && overlap_ssms; depth++) {
-        for (size_t s = 0; s < n; s++) {
+        for (int s : loc) {
           if (!inflight[s]) continue;
           inflight[s] = false;
           const ffmi_status cs = ssm_models[s]->beam_collect(beam_ir);
@@ -1354,6 +1468,7 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
           if (st != FFMI_OK) continue;  // collect the rest: no step left in flight
           stats.ssm_steps++;
           const double tp = now_us();  // (host scheduling: not SSM step time)
+          record_step(s, depth, (*beam_vec)[s], *beam_ir);
           (*beam_vec)[s] = prepare_next_batch_beam((*beam_vec)[s], *beam_ir);
           prep_us += now_us() - tp;
           if (depth + 1 < BeamSearchBatchConfig::MAX_BEAM_DEPTH) {
@@ -1365,6 +1480,12 @@ ffmi_status RequestManager::serve_spec_infer(ffmi_model *llm) {
       stats.ssm_us += now_us() - ts - prep_us;
     }
     if (st != FFMI_OK) break;
+    if (xch_world > 1) {  // the other ranks' SSMs (config E placement)
+      const double tx = now_us();
+      st = exchange_and_replay(beam_vec, beam_ir);
+      stats.ssm_exchange_us += now_us() - tx;
+      if (st != FFMI_OK) break;
+    }
     *tree_bc = prepare_next_batch_verify(*beam_vec);
     if (tree_bc->num_tokens == 0 && !all_done()) {
       st = FFMI_ERR_INVALID;

@@ -79,9 +79,22 @@ class RequestManager {
     bos_token_id = bos;
     eos_token_ids = eos;
   }
+  // m == nullptr: an SSM that runs on another rank of the TP group
+  // (set_ssm_exchange); every rank registers the same SSMs in the same order
   int register_ssm_model(ffmi_model *m) {
     ssm_models.push_back(m);
     return (int)ssm_models.size() - 1;
+  }
+  // Config E's SSMs placed over the ranks of a TP group: SSM s runs on rank
+  // s % nranks only (the reference builds each SSM as its own TP = 1 model,
+  // spec_infer.cc:381-435).  After its SSMs' beam steps each rank contributes
+  // their per-step results through `fn` (an all-gather of equal-size byte
+  // blocks: fn(ctx, mine, bytes, all[nranks][bytes]) == 0 on success) and
+  // replays the other ranks' SSMs' bookkeeping on theirs, so every rank
+  // merges the identical trees.
+  typedef int (*AllGather)(void *ctx, const void *mine, size_t bytes, void *all);
+  void set_ssm_exchange(int nranks, int rank, AllGather fn, void *ctx) {
+    xch_world = nranks, xch_rank = rank, xch_fn = fn, xch_ctx = ctx;
   }
   size_t get_num_ssms() const { return ssm_models.size(); }
   // register_output_filepath (request_manager.cc:246-249): every completed
@@ -145,6 +158,12 @@ class RequestManager {
   // replayed on the results (identical batches and trees)
   ffmi_status run_ssm_phase_chained(std::vector<BeamSearchBatchConfig> *beam_vec,
                                     BeamInferenceResult *beam_ir);
+  // distributed SSMs: keep a local SSM's step results / exchange them and
+  // replay the remote SSMs' prepare_next_batch_beam chains
+  void record_step(int s, int depth, const BeamSearchBatchConfig &bc,
+                   const BeamInferenceResult &ir);
+  ffmi_status exchange_and_replay(std::vector<BeamSearchBatchConfig> *beam_vec,
+                                  BeamInferenceResult *beam_ir);
 
   bool all_done() const;
   const GenerationResult *get_generation_result(RequestGuid guid) const;
@@ -163,6 +182,7 @@ class RequestManager {
     double wall_us = 0;
     double llm_us = 0, ssm_us = 0;  // wall time inside the model steps (incl. sync)
     long ssm_phases_chained = 0;
+    double ssm_exchange_us = 0;  // distributed SSMs: exchange + replay
   } stats;
 
  private:
@@ -201,6 +221,16 @@ class RequestManager {
   std::vector<BeamSearchBatchConfig> chain_spec;  // staged chained beam batches
   std::unique_ptr<BeamInferenceResult> chain_ph;   // placeholder results (-1 - i)
   double chain_t[5] = {};  // (FFMI_STEP_TIMING: host-side phase timings, count)
+  // distributed SSMs (set_ssm_exchange)
+  int xch_world = 1, xch_rank = 0;
+  AllGather xch_fn = nullptr;
+  void *xch_ctx = nullptr;
+  std::vector<int> ssm_local;  // indices of the SSMs this rank runs
+  struct StepRecord {
+    std::vector<int> ids;
+    std::vector<float> probs;
+  };
+  std::vector<std::vector<StepRecord>> phase_rec;  // [ssm][depth] of the phase
 };
 
 double now_us();

@@ -119,8 +119,11 @@ class ServeStats(ctypes.Structure):
     _fields_ = [("llm_steps", c_long), ("ssm_steps", c_long), ("tokens_committed", c_long),
                 ("tree_tokens_verified", c_long), ("request_verifies", c_long),
                 ("wall_us", c_double), ("llm_us", c_double), ("ssm_us", c_double),
-                ("ssm_phases_chained", c_long)]
+                ("ssm_phases_chained", c_long), ("ssm_exchange_us", c_double)]
 
+
+# ffmi_allgather_fn (include/ffmi.h): an all-gather of equal-size host blocks
+ALLGATHER_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_void_p, c_size_t, c_void_p)
 
 # name -> (restype, argtypes); every symbol declared in include/ffmi.h
 SIGNATURES = {
@@ -183,6 +186,10 @@ SIGNATURES = {
     "ffmi_rm_create": (c_int, [ctypes.POINTER(RMConfig), ctypes.POINTER(c_void_p)]),
     "ffmi_rm_destroy": (None, [c_void_p]),
     "ffmi_rm_register_ssm": (c_int, [c_void_p, c_void_p]),
+    "ffmi_rm_register_remote_ssm": (c_int, [c_void_p]),
+    "ffmi_rm_set_ssm_exchange": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p]),
+    "ffmi_rm_set_ssm_exchange_comm": (c_int, [c_void_p, c_void_p]),
+    "ffmi_comm_allgather": (c_int, [c_void_p, c_void_p, c_size_t, c_void_p]),
     "ffmi_rm_register_output_filepath": (c_int, [c_void_p, ctypes.c_char_p]),
     "ffmi_rm_register_detokenizer": (c_int, [c_void_p, c_void_p, c_void_p]),
     "ffmi_rm_set_old_llama_tokenizer": (c_int, [c_void_p, c_int]),

@@ -216,9 +216,42 @@ class RequestManager:
     def __del__(self):
         self.close()
 
-    def register_ssm_model(self, ssm: Model):
-        F.check(F.lib().ffmi_rm_register_ssm(self.handle, ssm.handle), "register ssm")
+    def register_ssm_model(self, ssm: Optional[Model]):
+        """ssm=None: an SSM that another rank of the TP group runs (config E's
+        placement, set_ssm_exchange): every rank registers the same SSMs in
+        the same order, SSM s as a model on rank s % nranks only."""
+        if ssm is None:
+            F.check(F.lib().ffmi_rm_register_remote_ssm(self.handle), "register remote ssm")
+        else:
+            F.check(F.lib().ffmi_rm_register_ssm(self.handle, ssm.handle), "register ssm")
         self._ssms.append(ssm)
+
+    def set_ssm_exchange(self, exchange, nranks: int = 1, rank: int = 0):
+        """Distributed SSMs (include/ffmi.h ffmi_rm_set_ssm_exchange): after
+        its SSMs' beam steps each rank exchanges their results and replays
+        the other ranks' SSMs' bookkeeping.  `exchange` is a Comm (its all-
+        gather over the TP transport) or a callable all_gather(bytes) ->
+        list of every rank's bytes (e.g. torch.distributed over gloo)."""
+        if isinstance(exchange, Comm):
+            F.check(F.lib().ffmi_rm_set_ssm_exchange_comm(self.handle, exchange.handle),
+                    "ssm exchange")
+            self._xch = exchange
+            return
+
+        def fn(_ctx, mine, nbytes, out):
+            try:
+                parts = exchange(ctypes.string_at(mine, nbytes))
+                if len(parts) != nranks or any(len(p) != nbytes for p in parts):
+                    return 1
+                ctypes.memmove(out, b"".join(parts), nbytes * nranks)
+                return 0
+            except Exception:  # never unwind a Python error through C++
+                return 1
+
+        self._xch = F.ALLGATHER_FN(fn)  # kept alive with the manager
+        F.check(F.lib().ffmi_rm_set_ssm_exchange(self.handle, nranks, rank,
+                                                 ctypes.cast(self._xch, ctypes.c_void_p), None),
+                "ssm exchange")
 
     def register_output_filepath(self, path: Optional[str]):
         """RequestManager::register_output_filepath (request_manager.cc:246-249):

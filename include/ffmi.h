@@ -269,6 +269,10 @@ ffmi_status ffmi_comm_create_peer(int nranks, int rank, ffmi_comm **out);
 ffmi_status ffmi_comm_peer_export(ffmi_comm *c, size_t max_bytes,
                                   void *handle_out /* FFMI_PEER_HANDLE_BYTES */);
 ffmi_status ffmi_comm_peer_attach(ffmi_comm *c, const void *handles /* [nranks][64] */);
+/* All-gather of equal-size HOST byte blocks over the communicator (any of its
+ * transports): all[r * bytes ...] = rank r's block, on every rank.  Blocking;
+ * for control data (the distributed SSMs' results), not the hot path. */
+ffmi_status ffmi_comm_allgather(ffmi_comm *c, const void *mine, size_t bytes, void *all);
 ffmi_status ffmi_comm_peer_status(ffmi_comm *c);
 /* Stop using the transport (RCCL again): for a control plane that saw some
  * rank fail its attach -- every rank must take the same transport. */
@@ -492,6 +496,21 @@ typedef struct {
 ffmi_status ffmi_rm_create(const ffmi_rm_config *cfg, ffmi_rm **out);
 void ffmi_rm_destroy(ffmi_rm *rm);
 ffmi_status ffmi_rm_register_ssm(ffmi_rm *rm, ffmi_model *ssm);
+/* Config E's SSMs placed over the ranks of a TP group (the reference builds
+ * each SSM as its own TP = 1 model, spec_infer.cc:381-435): SSM s runs on
+ * rank s % nranks only.  Every rank registers the SSMs in the same order --
+ * its own with ffmi_rm_register_ssm, the others with
+ * ffmi_rm_register_remote_ssm -- and sets an exchange.  After its SSMs' beam
+ * steps a rank contributes their per-step results and replays the other
+ * ranks' SSMs' bookkeeping on theirs, so every rank merges the identical token
+ * trees (FFMI_SPEC_EXT_MULTI_SSM).  The exchange is an all-gather of equal-
+ * size host byte blocks, fn(ctx, mine, bytes, all[nranks][bytes]) returning
+ * 0 on success; ffmi_rm_set_ssm_exchange_comm uses ffmi_comm_allgather. */
+typedef int (*ffmi_allgather_fn)(void *ctx, const void *mine, size_t bytes, void *all);
+ffmi_status ffmi_rm_register_remote_ssm(ffmi_rm *rm);
+ffmi_status ffmi_rm_set_ssm_exchange(ffmi_rm *rm, int nranks, int rank, ffmi_allgather_fn fn,
+                                     void *ctx);
+ffmi_status ffmi_rm_set_ssm_exchange_comm(ffmi_rm *rm, ffmi_comm *comm);
 /* RequestManager::register_output_filepath (request_manager.cc:246-249):
  * each completed request is appended in the reference's record format
  * (incr decoding :813-840, SpecInfer :1303-1330).  NULL or "" turns it off. */
@@ -533,6 +552,7 @@ typedef struct {
   double wall_us;
   double llm_us, ssm_us; /* wall time inside LLM / SSM steps; the rest is host scheduling */
   long ssm_phases_chained; /* speculation phases run as chained beam steps (FFMI_SSM_CHAIN) */
+  double ssm_exchange_us;  /* distributed SSMs: result exchange + remote bookkeeping */
 } ffmi_serve_stats;
 ffmi_status ffmi_rm_get_stats(ffmi_rm *rm, ffmi_serve_stats *s);
 

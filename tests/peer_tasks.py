@@ -111,7 +111,7 @@ def vshard_task(fa, comm, rank, n, T, V, k, seed):
 
 
 def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ssm_cfg,
-                     tf_seqs=(), weight_init=0, fault=None):
+                     tf_seqs=(), weight_init=0, fault=None, ssm_place="replicated"):
     """One TP shard per rank of a full-depth model over the xGMI transport:
     incr decoding (spec False) or SpecInfer with the SSM replicated on every
     rank (spec_infer.cc:385-387).  Then, in incr mode, a teacher-forced pass:
@@ -127,14 +127,20 @@ def tp_generate_task(fa, comm, rank, n, cfg, seed, prompts, max_length, spec, ss
     mtb = 256
     if spec:  # True or a tests/spec_configs.py name; the SSMs replicated per rank
         from spec_configs import spec_setup
+        # ssm_place "distributed": SSM s on rank s % n only, results exchanged
+        # (config E's placement); "replicated": every SSM on every rank
+        place = (comm, rank, n) if ssm_place == "distributed" else None
         rm, ssms, vt, tt = spec_setup("w113" if spec is True else spec, ssm_cfg, B, mtb, 128,
-                                      weight_init=weight_init)
+                                      place=place, weight_init=weight_init)
         m = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=128,
                      max_tree_tokens=tt, weight_seed=seed, tp_rank=rank, tp_size=n, comm=comm,
                      weight_init=weight_init)
         apply_fault(m)
         res = fa.generate(rm, m, prompts, max_length=max_length, spec=True)
-        out = {"tokens": [r.output_tokens for r in res], "llm_steps": rm.stats().llm_steps}
+        st = rm.stats()
+        out = {"tokens": [r.output_tokens for r in res], "llm_steps": st.llm_steps,
+               "ssm_steps": st.ssm_steps, "tree_tokens_verified": st.tree_tokens_verified,
+               "ssm_us": st.ssm_us, "ssm_exchange_us": st.ssm_exchange_us}
         m.close()
         for x in ssms:
             x.close()

@@ -19,18 +19,27 @@ SPEC = {
 }
 
 
-def spec_setup(name, ssm_cfg, B, mtb, max_seq, **model_kw):
+def spec_setup(name, ssm_cfg, B, mtb, max_seq, place=None, **model_kw):
     """RequestManager with config `name`'s widths / extensions, its SSMs
     registered.  Returns (rm, ssms, vt, tree): vt = the verify batch's token
-    capacity (mtb + tree * B), the LLM's max_tokens."""
+    capacity (mtb + tree * B), the LLM's max_tokens.  place = (comm, rank,
+    nranks): the SSMs distributed over the TP group (SSM s on rank s % nranks,
+    ffmi_rm_set_ssm_exchange_comm); otherwise every SSM is built here."""
     sc = SPEC[name]
     tree = sc["tree"]
     vt = mtb + tree * B
     rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
                            max_sequence_length=max_seq, spec_tree_width=sc["widths"],
                            max_spec_tree_token_num=tree, spec_extensions=sc["ext"])
-    ssms = [fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=vt, max_seq_len=max_seq,
-                     max_tree_tokens=tree, weight_seed=s, **model_kw) for s in sc["ssm_seeds"]]
-    for s in ssms:
-        rm.register_ssm_model(s)
+    ssms = []
+    for i, seed in enumerate(sc["ssm_seeds"]):
+        if place is not None and i % place[2] != place[1]:
+            rm.register_ssm_model(None)  # another rank runs it
+            continue
+        m = fa.Model(ssm_cfg, "beam", max_requests=B, max_tokens=vt, max_seq_len=max_seq,
+                     max_tree_tokens=tree, weight_seed=seed, **model_kw)
+        ssms.append(m)
+        rm.register_ssm_model(m)
+    if place is not None:
+        rm.set_ssm_exchange(place[0])
     return rm, ssms, vt, tree

@@ -183,6 +183,35 @@ def test_llama65b_80L_tp8_processes_vs_tp1(weight_init, spec_cfg):
         # of the TP = 8 sequences' teacher-forced rows (checked above)
 
 
+@pytest.mark.parametrize("weight_init", ["token_chain", "uniform"])
+def test_llama65b_80L_tp8_ssms_distributed_equal_replicated(weight_init):
+    """Config E's four SSMs placed one per rank (SSM s on rank s % 8; ranks
+    4-7 run none), their beam-step results exchanged over the TP transport
+    (ffmi_rm_set_ssm_exchange_comm) and the remote SSMs' bookkeeping replayed:
+    the merged trees, verify steps and tokens must be IDENTICAL to every rank
+    running all four SSMs (same kernels, same inputs), on every rank, and each
+    rank must run only its SSM's steps."""
+    ps = prompts()
+    max_length = len(ps[0]) + 1 + NEW
+    kw = dict(max_bytes=(512 + 64 * 3 + 16) * 8192 * 2, timeout=900)
+    rep = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, "ssm4", LLAMA_68M,
+                                              (), weight_init, None, "replicated"), **kw)
+    dis = run_group(TP, PT.tp_generate_task, (LLAMA_65B, SEED, ps, max_length, "ssm4", LLAMA_68M,
+                                              (), weight_init, None, "distributed"), **kw)
+    for r in range(TP):
+        assert dis[r]["tokens"] == rep[0]["tokens"], r
+        assert dis[r]["llm_steps"] == rep[0]["llm_steps"], r
+        assert dis[r]["tree_tokens_verified"] == rep[0]["tree_tokens_verified"], r
+    per_ssm = rep[0]["ssm_steps"] // 4
+    assert [d["ssm_steps"] for d in dis] == [per_ssm] * 4 + [0] * 4
+    report(f"llama65b_tp8_ssms_distributed_{weight_init}",
+           replicated_ssm_steps=rep[0]["ssm_steps"], distributed_ssm_steps=dis[0]["ssm_steps"],
+           replicated_ssm_ms=round(rep[0]["ssm_us"] / 1e3, 1),
+           distributed_ssm_ms=[round(d["ssm_us"] / 1e3, 1) for d in dis],
+           exchange_ms=[round(d["ssm_exchange_us"] / 1e3, 1) for d in dis],
+           llm_steps=rep[0]["llm_steps"])
+
+
 def test_llama65b_80L_tp8_negative_controls():
     """The TP path's own negative controls (ffmi_model_debug_fault, applied to
     ONE rank's shard of the 80-layer LLaMA-65B at TP = 8): tp_rule must
