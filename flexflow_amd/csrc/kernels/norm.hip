@@ -740,7 +740,7 @@ __global__ __launch_bounds__(TPB) void softmax_topk_kernel(
 // split-row workspace: [kSplitRows] row counters at a FIXED offset (one
 // workspace serves steps of every T: a counter must never share bytes with
 // another T's partials), then [T][G <= 16] partial sums
-constexpr int kSplitRows = 128;
+constexpr int kSplitRows = 256;
 constexpr size_t kSplitPartOff = kSplitRows * 4;
 size_t argmax_workspace_bytes(int T) {
   return T <= 0 ? 0 : kSplitPartOff + (size_t)std::min(T, kSplitRows) * 16 * 8;
@@ -753,7 +753,12 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   // workgroups per row (the split form needs the caller's zeroed workspace):
   // T x G <= 256, one workgroup per CU; FFMI_TOPK_SPLIT = 0 (off) / G (forced)
   static const int split_env = getenv("FFMI_TOPK_SPLIT") ? atoi(getenv("FFMI_TOPK_SPLIT")) : -1;
-  int G = T <= 16 ? 16 : T <= 32 ? 8 : T <= 64 ? 4 : T <= kSplitRows ? 2 : 1;
+  // (T 129-256, the verify step's argmax, two workgroups per row with
+  // FFMI_TOPK_SPLIT2=1: measured slower, 20.0 vs 13.1 us at T = 168 after the
+  // lm_head GEMM -- 336 workgroups put two on many CUs -- and the verify step
+  // 5.30 vs 5.28 ms; off)
+  static const bool split2 = getenv("FFMI_TOPK_SPLIT2") && atoi(getenv("FFMI_TOPK_SPLIT2"));
+  int G = T <= 16 ? 16 : T <= 32 ? 8 : T <= 64 ? 4 : T <= 128 ? 2 : (T <= kSplitRows && split2) ? 2 : 1;
   if (split_env >= 0) G = split_env;
   if (!ws || ws_bytes < argmax_workspace_bytes(T) || T > kSplitRows) G = 1;
   unsigned *cnt = reinterpret_cast<unsigned *>(ws);

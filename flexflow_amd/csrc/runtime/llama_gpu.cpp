@@ -543,7 +543,7 @@ struct LlamaGPU : public ffmi_model {
     TRY(alloc(&logits, (size_t)Tm * Vl));
     if (Vl != V) TRY(alloc(&xch, (ffmi_vocab_shard_scratch_bytes(P, Tm) + 3) / 4));
     TRY(alloc(&ids_d, (size_t)Tm * 4 * 2));  // [ids | probs] of a step, one D2H copy
-    topk_ws_bytes = ffmi::argmax_workspace_bytes(std::min(Tm, 128));
+    topk_ws_bytes = ffmi::argmax_workspace_bytes(std::min(Tm, 256));
     TRY(alloc((char **)&topk_ws, topk_ws_bytes));
     FFMI_HIP(hipMemsetAsync(topk_ws, 0, topk_ws_bytes, stream));
     peer = P > 1 && ffmi::comm_has_peer(o.comm, (size_t)Tm * H * 2);
@@ -1203,13 +1203,17 @@ struct LlamaGPU : public ffmi_model {
     ffmi_status st = forward_launch(k);
     batch = chain_batch[0];
     cur_slot = 0;
-    // per-slot events let the scheduler replay slot d while later slots run,
-    // but each costs the GPU more than the replay it overlaps (same-box A/B,
-    // tokens/s: 1342 without, 1333 with, 1326 stepwise): off unless
-    // FFMI_CHAIN_EVENTS=1; the collect then waits for the whole chain
-    static const bool slot_events = getenv("FFMI_CHAIN_EVENTS") && atoi(getenv("FFMI_CHAIN_EVENTS"));
-    if (st == FFMI_OK && !slot_events) last_slot = slot;
-    if (st == FFMI_OK && slot_events) {
+    // Events let the scheduler replay slot d's bookkeeping while later slots
+    // run.  One behind every slot cost the GPU more than the replay it
+    // overlapped (same-box A/B, tokens/s: 1333 with, 1342 with none, 1326
+    // stepwise); FFMI_CHAIN_EVENTS: 0 none (the collect waits for the whole
+    // chain), 1 every slot, 2 (default) one, behind the second-to-last slot:
+    // the replays of slots 0 .. D-2 then run while slot D-1 computes
+    static const int slot_events =
+        getenv("FFMI_CHAIN_EVENTS") ? atoi(getenv("FFMI_CHAIN_EVENTS")) : 2;
+    const bool record = slot_events == 1 || (slot_events == 2 && slot == kChain - 2);
+    if (st == FFMI_OK) last_slot = slot;
+    if (st == FFMI_OK && record) {
       // (so that the scheduler can collect this slot while later ones run)
       if (!slot_ev[slot])
         FFMI_HIP(hipEventCreateWithFlags(&slot_ev[slot], step_timing ? 0 : hipEventDisableTiming));
@@ -1221,9 +1225,12 @@ struct LlamaGPU : public ffmi_model {
   }
   ffmi_status beam_collect_chained(int slot, BeamInferenceResult *ir) override {
     FFMI_CHECK(slot >= 0 && slot < kChain, FFMI_ERR_INVALID);
-    if (slot < last_slot && slot_ev[slot] && slot_ev_live[slot]) {
-      // later slots still run: wait for this one only
-      FFMI_HIP(hipEventSynchronize(slot_ev[slot]));
+    int ev = -1;  // the first live event at or after this slot, before the last
+    for (int e = slot; e < last_slot && ev < 0; ++e)
+      if (slot_ev_live[e] && slot_ev[e]) ev = e;
+    if (ev >= 0) {
+      // later slots still run: wait for this one (and those before it) only
+      FFMI_HIP(hipEventSynchronize(slot_ev[ev]));
     } else {
       const int ls = last_slot;
       ffmi_status st = forward_finish();  // (every launched step: one stream)

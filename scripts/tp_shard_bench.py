@@ -28,6 +28,9 @@ def main():
     ap.add_argument("--steps", type=int, default=1)
     ap.add_argument("--model", choices=["7b", "65b"], default="7b")
     ap.add_argument("--mode", choices=["spec", "incr"], default="spec")
+    ap.add_argument("--ssms", type=int, default=1,
+                    help="SSMs on this rank (4: config E's SSMs replicated per rank; 1: this "
+                         "rank's share when they are distributed one per rank)")
     args = ap.parse_args()
     cfg = LLAMA_65B if args.model == "65b" else LLAMA_7B
     spec = args.mode == "spec"
@@ -39,29 +42,45 @@ def main():
     if spec:
         llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=mtb + tree * B, max_seq_len=512,
                        max_tree_tokens=tree, tp_rank=0, tp_size=args.tp, comm=comm)
-        ssm = fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=mtb + tree * B,
-                       max_seq_len=512, max_tree_tokens=tree, weight_seed=68)
-        rm = fa.RequestManager(spec_tree_width=(1, 1, 3), **rm_kw)
-        rm.register_ssm_model(ssm)
+        if args.ssms > 1:  # config E: merged trees up to 64 tokens
+            rm_kw["max_spec_tree_token_num"] = tree = 64
+            llm.close()
+            llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=mtb + tree * B,
+                           max_seq_len=512, max_tree_tokens=tree, tp_rank=0, tp_size=args.tp,
+                           comm=comm)
+        ssms = [fa.Model(LLAMA_68M, "beam", max_requests=B, max_tokens=mtb + tree * B,
+                         max_seq_len=512, max_tree_tokens=tree, weight_seed=68 + i)
+                for i in range(args.ssms)]
+        rm = fa.RequestManager(spec_tree_width=(1, 1, 3),
+                               spec_extensions=fa.ffmi.SPEC_EXT_MULTI_SSM if args.ssms > 1 else 0,
+                               **rm_kw)
+        for ssm in ssms:
+            rm.register_ssm_model(ssm)
     else:
         llm = fa.Model(cfg, "inc", max_requests=B, max_tokens=mtb, max_seq_len=512,
                        tp_rank=0, tp_size=args.tp, comm=comm)
         rm = fa.RequestManager(**rm_kw)
     prompts = make_prompts(B, P - 1, cfg["vocab_size"])
     fa.generate(rm, llm, prompts, max_length=P + D)  # warm
-    llm.set_profiling(1)
     t0 = time.time()
-    for _ in range(args.steps):
+    llm_us = ssm_us = 0.0
+    for _ in range(args.steps):  # timed with op profiling off, as the bench
         res = fa.generate(rm, llm, prompts, max_length=P + D)
+        st = rm.stats()
+        llm_us += st.llm_us
+        ssm_us += st.ssm_us
     dt = (time.time() - t0) / args.steps
-    st = rm.stats()
+    llm.set_profiling(1)  # op breakdown: one more, untimed generate
+    fa.generate(rm, llm, prompts, max_length=P + D)
     ops = llm.op_stats()
+    llm.set_profiling(0)
     print(json.dumps({
-        "model": args.model, "mode": args.mode, "tp": args.tp, "s_per_generate": round(dt, 3),
+        "model": args.model, "mode": args.mode, "tp": args.tp, "ssms": args.ssms if spec else 0,
+        "s_per_generate": round(dt, 3),
         "tokens_per_s_without_allreduce": round(sum(len(r.output_tokens) - len(r.input_tokens)
                                                     for r in res) / dt, 1),
-        "llm_ms": round(st.llm_us / 1000 / (args.steps + 1), 1),
-        "ssm_ms": round(st.ssm_us / 1000 / (args.steps + 1), 1),
+        "llm_ms": round(llm_us / 1000 / args.steps, 1),
+        "ssm_ms": round(ssm_us / 1000 / args.steps, 1),
         "ops_avg_us": {k: round(1000 * v["ms"] / v["launches"], 2) for k, v in ops.items()},
     }))
 

@@ -449,7 +449,7 @@ class TopkWs:
         return not self.buf.get()[:T].any()
 
 
-@pytest.mark.parametrize("T", [1, 5, 8, 16, 17, 24, 32, 33, 64, 65, 100, 128])
+@pytest.mark.parametrize("T", [1, 5, 8, 16, 17, 24, 32, 33, 64, 65, 100, 128, 129, 168, 256])
 @pytest.mark.parametrize("V", [4104, 8000, 16000, 32000])
 def test_softmax_topk_split_rows_exact(T, V):
     """The split-row form (ffmi_arg_topk_ws: T <= 128 rows over 2-16
@@ -465,7 +465,7 @@ def test_softmax_topk_split_rows_exact(T, V):
         m = f16(float(np.abs(logits[t]).max()) + 1.0)
         logits[t, rng.choice(V, size=3, replace=False)] = m
     lb = Buf(logits)
-    ws = TopkWs(128)
+    ws = TopkWs(256)
     for k in (1, 2, 3, 4):
         rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
         for _ in range(2):
@@ -483,8 +483,8 @@ def test_softmax_topk_split_one_workspace_many_shapes():
     the counters of a later step with more rows (round 6: they did, and the
     next step found no last workgroup -- stale ids)."""
     rng = np.random.default_rng(31337)
-    ws = TopkWs(128)
-    for T in (40, 100, 8, 128, 33, 17, 64, 1, 120, 24, 24, 65, 9):
+    ws = TopkWs(256)
+    for T in (40, 100, 8, 128, 33, 17, 64, 1, 120, 24, 24, 65, 9, 168, 256, 130):
         V = 32000
         logits = f16(rng.standard_normal((T, V)) * 2.0)
         lb = Buf(logits)
@@ -494,7 +494,7 @@ def test_softmax_topk_split_one_workspace_many_shapes():
         rid, rp = O.softmax_topk(logits.astype(np.float32), k, fp16=1)
         assert np.array_equal(ids.get(), rid.reshape(T, k)), T
         np.testing.assert_array_equal(pr.get(), rp.reshape(T, k))
-        assert ws.counters_zero(128), T
+        assert ws.counters_zero(256), T
 
 
 @pytest.mark.parametrize("seed", range(6 * RS))
@@ -503,7 +503,7 @@ def test_softmax_topk_split_random_exact(seed):
     of 8 up to 32768, planted ties), bit-exact against the oracle and against
     the one-workgroup form."""
     rng = np.random.default_rng(4242 + OFF + seed)
-    T = int(rng.integers(1, 129))
+    T = int(rng.integers(1, 257))
     V = 8 * int(rng.integers(8, 4097))
     scale = float(rng.choice([1e-3, 0.05, 1.0, 3.0, 8.0]))
     logits = f16(rng.standard_normal((T, V)) * scale)
