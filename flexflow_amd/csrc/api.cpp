@@ -900,7 +900,9 @@ extern "C" ffmi_status ffmi_comm_peer_export(ffmi_comm *c, size_t max_bytes, voi
 
 static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows, size_t cols,
                             size_t ld, size_t col0, int dtype, hipStream_t s,
-                            const ffmi::Partials *slabs = nullptr) {
+                            const ffmi::Partials *slabs = nullptr, int rs_row0 = -1,
+                            int rs_row1 = -1, const ffmi::PeerNormArgs *norm = nullptr,
+                            int two_shot = -1) {
   PeerState &p = *c->peer;
   const size_t esz = dtype == FFMI_F16 ? 2 : 4;
   const size_t bytes = rows * cols * esz;
@@ -928,7 +930,9 @@ static ffmi_status peer_run(ffmi_comm *c, const void *in, void *out, size_t rows
   a.err = p.err_d;
   a.timeout_ticks = p.timeout_ticks;
   if (slabs && slabs->S > 0) a.slabs = slabs->p, a.S = slabs->S, a.NP = slabs->NP, a.rows = rows;
-  FFMI_HIP(ffmi::launch_peer_allreduce(a, bytes >= p.two_shot_min, s));
+  const bool ts = two_shot >= 0 ? two_shot != 0 : bytes >= p.two_shot_min;
+  if (norm) FFMI_HIP(ffmi::launch_peer_allreduce_norm(a, *norm, ts, s));
+  else FFMI_HIP(ffmi::launch_peer_allreduce(a, ts, s, rs_row0, rs_row1));
   return FFMI_OK;
 }
 
@@ -1026,6 +1030,30 @@ ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int row
                                 int ld, int col0, int dtype, hipStream_t s, const Partials *slabs) {
   return peer_run(c, in, out, rows, cols, ld, col0, dtype, s, slabs);
 }
+bool comm_two_shot(const ffmi_comm *c, size_t bytes) {
+  return c && c->peer && c->peer->attached && c->nranks > 1 && bytes >= c->peer->two_shot_min;
+}
+ffmi_status comm_reduce_rows(ffmi_comm *c, const void *in, void *out, int rows, int cols, int ld,
+                             int col0, int row0, int row1, hipStream_t s, const Partials *slabs) {
+  return peer_run(c, in, out, rows, cols, ld, col0, FFMI_F16, s, slabs, row0, row1, nullptr, 1);
+}
+ffmi_status comm_allreduce_norm(ffmi_comm *c, const void *in, int T, int H, int col0,
+                                const uint16_t *prev, uint16_t *res, const uint16_t *w, float eps,
+                                uint16_t *h, bool packed, bool two_shot, hipStream_t s,
+                                const Partials *slabs) {
+  FFMI_CHECK(c && c->peer && c->peer->attached && res && w && h && T >= 0 && H > 0 && col0 >= 0 &&
+                 col0 < H,
+             FFMI_ERR_INVALID);
+  if (T == 0) return FFMI_OK;
+  ffmi::PeerNormArgs n;
+  n.res = res, n.w = w, n.h = h, n.prev = prev, n.T = T, n.H = H, n.packed = packed ? 1 : 0;
+  n.eps = eps;
+  n.row0 = two_shot ? (int)((long)T * c->rank / c->nranks) : 0;
+  n.row1 = two_shot ? (int)((long)T * (c->rank + 1) / c->nranks) : T;
+  // (in: [T][H - col0]; out unused -- h and res are the outputs)
+  return peer_run(c, in, h, T, H - col0, H - col0, col0, FFMI_F16, s, slabs, -1, -1, &n,
+                  two_shot ? 1 : 0);
+}
 ffmi_status comm_status(ffmi_comm *c) {
   return c && c->peer && c->peer->attached ? ffmi_comm_peer_status(c) : FFMI_OK;
 }
@@ -1092,6 +1120,32 @@ extern "C" ffmi_status ffmi_allreduce(ffmi_comm *c, const void *in, void *out, s
     return FFMI_ERR_NCCL;
   }
   return FFMI_OK;
+}
+
+extern "C" ffmi_status ffmi_allreduce_rmsnorm(ffmi_comm *c, const void *in, int T, int H,
+                                              int col0, const void *prev, void *residual,
+                                              const void *w, float eps, void *out, int flags,
+                                              int *rows_out, ffmi_stream stream) {
+  FFMI_CHECK(c && in && residual && w && out && T >= 0 && H > 0 && col0 >= 0 && col0 < H &&
+                 (col0 == 0 || prev) && (flags & ~FFMI_Y_PACKED) == 0,
+             FFMI_ERR_INVALID);
+  if (!(c->nranks > 1 && c->peer && c->peer->attached)) {
+    ffmi_set_last_error("ffmi_allreduce_rmsnorm needs an attached xGMI transport of >= 2 ranks",
+                        __FILE__, __LINE__);
+    return FFMI_ERR_UNSUPPORTED;
+  }
+  FFMI_CHECK(H % 8 == 0 && col0 % 8 == 0 && H / 8 <= 4096 &&
+                 (!(flags & FFMI_Y_PACKED) || H % 32 == 0),
+             FFMI_ERR_UNSUPPORTED);
+  FFMI_CHECK((size_t)T * H * 2 <= c->peer->cap, FFMI_ERR_INVALID);
+  const bool two = ffmi::comm_two_shot(c, (size_t)T * H * 2);
+  if (rows_out) {
+    rows_out[0] = two ? (int)((long)T * c->rank / c->nranks) : 0;
+    rows_out[1] = two ? (int)((long)T * (c->rank + 1) / c->nranks) : T;
+  }
+  return ffmi::comm_allreduce_norm(c, in, T, H, col0, (const uint16_t *)prev,
+                                   (uint16_t *)residual, (const uint16_t *)w, eps, (uint16_t *)out,
+                                   (flags & FFMI_Y_PACKED) != 0, two, (hipStream_t)stream);
 }
 
 extern "C" long ffmi_debug_gemm_stamps(long long *dst, long max_waves) {

@@ -42,8 +42,38 @@ struct PeerArgs {
   const float *slabs = nullptr;
   int S = 0;
   size_t NP = 0, rows = 0;
+  // reduce-scatter by rows (launch_peer_allreduce rs_rows): vectors [v0, v1)
+  size_t rs_v0 = 0, rs_v1 = 0;
 };
 
-hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s);
+// rs_rows: reduce-scatter by rows only -- rows [row0, row1) of the sum into
+// `out`, nothing published or gathered (the first column chunk of a fused
+// all-reduce + residual norm, launch_peer_allreduce_norm)
+hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s,
+                                 int rs_row0 = -1, int rs_row1 = -1);
+
+// All-reduce fused with the residual RMSNorm that follows it
+// (residual_rms_norm_kernels.cu:98-131 after allreduce_kernels.cu:53-75;
+// model.cc:3421-3470).  The all-reduced partial covers columns [col0, H) of
+// the [T][H] sum (PeerArgs cols = H - col0, f16); columns [0, col0) come from
+// `prev`, the sum of an earlier column chunk (launch_peer_allreduce with
+// rs_rows, or a whole one-shot all-reduce).  For rows [row0, row1):
+//   res = half(res + sum)   (in place)
+//   h   = RMSNorm(res) * w  (packed MFMA activation layout when `packed`)
+// with rmsnorm_kernel's arithmetic and reduction order, so h and res are
+// bit-identical to the all-reduce followed by the norm.  Two-shot: the rows
+// are this rank's share (T * r / N ..), h rows are published in the exchange
+// buffer and every rank gathers the others' -- h complete on every rank, res
+// valid on this rank's rows only.  One-shot: every rank computes every row.
+struct PeerNormArgs {
+  uint16_t *res = nullptr;        // [T][H]
+  const uint16_t *w = nullptr;    // [H]
+  uint16_t *h = nullptr;          // [T][H]
+  const uint16_t *prev = nullptr;  // [T][H] (columns < col0)
+  int T = 0, H = 0, packed = 0, row0 = 0, row1 = 0;
+  float eps = 0.f;
+};
+hipError_t launch_peer_allreduce_norm(const PeerArgs &a, const PeerNormArgs &n, bool two_shot,
+                                      hipStream_t s);
 
 }  // namespace ffmi

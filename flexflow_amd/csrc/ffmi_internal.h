@@ -298,6 +298,24 @@ bool comm_is_rccl(const ffmi_comm *c);
 ffmi_status comm_allreduce_cols(ffmi_comm *c, const void *in, void *out, int rows, int cols,
                                 int ld, int col0, int dtype, hipStream_t s,
                                 const Partials *slabs = nullptr);
+// the transport takes a message of `bytes` in two shots (reduce-scatter +
+// all-gather) rather than one
+bool comm_two_shot(const ffmi_comm *c, size_t bytes);
+// reduce-scatter by rows over the transport: rows [row0, row1) of the sum of
+// every rank's [rows][cols] into out (row stride ld, column offset col0);
+// must be followed by comm_allreduce_norm (two-shot) over the same rows
+ffmi_status comm_reduce_rows(ffmi_comm *c, const void *in, void *out, int rows, int cols, int ld,
+                             int col0, int row0, int row1, hipStream_t s,
+                             const Partials *slabs = nullptr);
+// all-reduce of every rank's [T][H - col0] partial (columns col0.. of the sum;
+// columns < col0 from prev) fused with the residual RMSNorm after it
+// (collective.h, PeerNormArgs): res += sum in place, h = norm(res) * w.
+// two_shot: this rank's rows T*r/N.. only, h gathered from the other ranks
+// (res valid on this rank's rows); else every row on every rank
+ffmi_status comm_allreduce_norm(ffmi_comm *c, const void *in, int T, int H, int col0,
+                                const uint16_t *prev, uint16_t *res, const uint16_t *w, float eps,
+                                uint16_t *h, bool packed, bool two_shot, hipStream_t s,
+                                const Partials *slabs = nullptr);
 // FFMI_OK, or the transport's timeout error after a synchronised step
 ffmi_status comm_status(ffmi_comm *c);
 ffmi_status attn_forward(ffmi_attn *h, const ffmi_batch_dev *b, const void *qkv, Partials qkvp,

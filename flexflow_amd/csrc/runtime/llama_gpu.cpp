@@ -93,6 +93,14 @@ struct LlamaGPU : public ffmi_model {
   bool fuse_ao = false;
   float *oslab = nullptr;
   int oslab_T = 0;
+  // the residual norm after each all-reduce folded into it over the transport
+  // (ffmi::comm_allreduce_norm; the reference's AllReduce -> ResidualRMSNorm,
+  // model.cc:3421-3470): no norm launch per all-reduce, and in two-shot mode
+  // each rank normalises only its T / N rows (res is then current on those
+  // rows only; h is complete).  FFMI_TP_FUSED_NORM: 0 off, 1 on (not with
+  // debug captures), 2 also with debug captures (tests: the h and logits
+  // captures are then of the fused path; o_proj / down / hidden are not kept)
+  int tp_fuse_norm = getenv("FFMI_TP_FUSED_NORM") ? atoi(getenv("FFMI_TP_FUSED_NORM")) : 1;
   int tp_chunks = 1;
   hipStream_t comm_stream = nullptr;
   uint16_t *chunk_buf = nullptr;  // [tp_chunks][Tm][H / tp_chunks]
@@ -768,6 +776,59 @@ struct LlamaGPU : public ffmi_model {
     return FFMI_OK;
   }
 
+  // rowpar_gemm_allreduce with the residual norm after it folded into the
+  // transport's all-reduce (tp_fuse_norm): res += sum (this rank's rows in
+  // two-shot mode), h = RMSNorm(res) * wnorm on every rank.  Column chunks:
+  // chunk 0 is reduced on comm_stream (two-shot: only this rank's rows) while
+  // chunk 1 computes; chunk 1's all-reduce carries the norm, reading chunk 0's
+  // columns of the sum from proj.
+  ffmi_status rowpar_gemm_allreduce_norm(const uint16_t *X, const uint16_t *W, int K, int T, int XP,
+                                         const uint16_t *wnorm) {
+    const int H = c.hidden;
+    const float eps = c.rms_eps;
+    const bool drop = ar_drop_now;
+    const bool two = ffmi::comm_two_shot(o.comm, (size_t)T * H * 2);
+    if (tp_chunks == 1) {
+      ffmi::Partials part;
+      FFMI_HIP(ffmi::launch_gemm(X, W, proj, ws, ws_bytes, T, H, K, XP, stream,
+                                 ar_slabs && !drop ? &part : nullptr));
+      if (drop) FFMI_HIP(hipMemsetAsync(proj, 0, (size_t)T * H * 2, stream));
+      return ffmi::comm_allreduce_norm(o.comm, proj, T, H, 0, nullptr, res, wnorm, eps, h, packed,
+                                       two, stream, part.S > 0 ? &part : nullptr);
+    }
+    const int Hc = H / tp_chunks;
+    const size_t tiles = (size_t)(Hc / 16) * ffmi::w_tile_stride((K + 31) / 32);
+    const int nr = ffmi::comm_size(o.comm), rk = ffmi::comm_rank(o.comm);
+    for (int ch = 0; ch < tp_chunks; ++ch) {
+      uint16_t *cb = chunk_buf + (size_t)ch * T * Hc;
+      ffmi::Partials part;
+      const bool def = ar_slabs && !drop;
+      FFMI_HIP(ffmi::launch_gemm(X, W + ch * tiles, cb,
+                                 def ? (float *)((char *)ws + ch * ws_chunk) : ws,
+                                 def ? ws_chunk : ws_bytes, T, Hc, K, XP, stream,
+                                 def ? &part : nullptr, H / 16));
+      if (drop) FFMI_HIP(hipMemsetAsync(cb, 0, (size_t)T * Hc * 2, stream));
+      FFMI_HIP(hipEventRecord(ev_chunk[ch], stream));
+      FFMI_HIP(hipStreamWaitEvent(comm_stream, ev_chunk[ch], 0));
+      const ffmi::Partials *sl = part.S > 0 ? &part : nullptr;
+      ffmi_status st;
+      if (ch + 1 < tp_chunks) {  // columns [ch Hc, (ch+1) Hc) of the sum into proj
+        st = two ? ffmi::comm_reduce_rows(o.comm, cb, proj, T, Hc, H, ch * Hc,
+                                          (int)((long)T * rk / nr), (int)((long)T * (rk + 1) / nr),
+                                          comm_stream, sl)
+                 : ffmi::comm_allreduce_cols(o.comm, cb, proj, T, Hc, H, ch * Hc, FFMI_F16,
+                                             comm_stream, sl);
+      } else {
+        st = ffmi::comm_allreduce_norm(o.comm, cb, T, H, ch * Hc, proj, res, wnorm, eps, h, packed,
+                                       two, comm_stream, sl);
+      }
+      if (st != FFMI_OK) return st;
+    }
+    FFMI_HIP(hipEventRecord(ev_comm_done, comm_stream));
+    FFMI_HIP(hipStreamWaitEvent(stream, ev_comm_done, 0));
+    return FFMI_OK;
+  }
+
   // One step over the packed batch; k = results per token.  Small batches
   // (SSM beam steps, decode) are launch-bound -- ~20 kernels of a few us
   // each -- so their whole step (metadata copy, kernels, result copies) is
@@ -938,6 +999,8 @@ struct LlamaGPU : public ffmi_model {
     int mark_i = 0;
     const bool fuse = (fuse_norms == 2 || (fuse_norms == 1 && H >= 2048)) && !dbg &&
                       o.tp_size == 1 && T <= 32 && H % 32 == 0 && Hl % 32 == 0 && H <= 4096;
+    // the residual norms inside the transport's all-reduces (tp_fuse_norm)
+    const bool arn = peer && !solo && o.tp_size > 1 && (tp_fuse_norm == 2 || (tp_fuse_norm == 1 && !dbg));
     for (int l = 0; l < c.num_layers; ++l) {
       Layer &L = layers[l];
       const bool on = prof_on(l, T);
@@ -968,7 +1031,7 @@ struct LlamaGPU : public ffmi_model {
         fz_qkv.wnorm = L.in_norm, fz_gu.wnorm = L.post_norm;
         fz_qkv.eps = fz_gu.eps = eps;
       }
-      if (!fz_in) {
+      if (!fz_in && !(arn && l > 0)) {  // (arn: the previous down all-reduce normalised)
         pr = prof_begin(on);
         // layer 0: the embedding lookup gathers straight into the first norm
         // (embedding_kernels.cu:233-244; res = the looked-up rows)
@@ -985,8 +1048,9 @@ struct LlamaGPU : public ffmi_model {
         mk();
       }
       if (dbg) {
-        // residual stream after layer l-1 (layer 0: the embedding rows)
-        TRY(dbg_copy(l == 0 ? FFMI_DBG_EMBED : FFMI_DBG_HIDDEN, l == 0 ? 0 : l - 1, res, T));
+        // residual stream after layer l-1 (layer 0: the embedding rows; arn:
+        // current on this rank's rows only, not kept)
+        if (l == 0 || !arn) TRY(dbg_copy(l == 0 ? FFMI_DBG_EMBED : FFMI_DBG_HIDDEN, l == 0 ? 0 : l - 1, res, T));
         TRY(dbg_copy(FFMI_DBG_ATTN_NORM, l, h, T));
       }
       pr = prof_begin(on);
@@ -1027,13 +1091,14 @@ struct LlamaGPU : public ffmi_model {
       } else {  // GEMM + all-reduce (overlapped over xGMI): timed together
         pr = prof_begin(on);
         ar_drop_now = l == ar_drop_layer && ar_drop_which == 0;
-        TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
+        if (arn) TRY(rowpar_gemm_allreduce_norm(att, L.wo, Hl, T, XP, L.post_norm));
+        else TRY(rowpar_gemm_allreduce(att, L.wo, Hl, proj, T, XP));
         ar_drop_now = false;
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Hl), 2.0 * T * H * Hl);
         mk();
       }
-      if (dbg) TRY(dbg_gemm_out(FFMI_DBG_O_PROJ, l, proj, o_part, T));
-      if (!fuse) {
+      if (dbg && !arn) TRY(dbg_gemm_out(FFMI_DBG_O_PROJ, l, proj, o_part, T));
+      if (!fuse && !arn) {
         pr = prof_begin(on);
         FFMI_HIP(ffmi::launch_rmsnorm(res, proj, L.post_norm, res, h, T, H, eps, stream, packed,
                                       o_part));
@@ -1068,12 +1133,16 @@ struct LlamaGPU : public ffmi_model {
       } else {
         pr = prof_begin(on);
         ar_drop_now = l == ar_drop_layer && ar_drop_which == 1;
-        TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
+        // (arn: the next layer's input norm, or the final norm, rides along)
+        if (arn)
+          TRY(rowpar_gemm_allreduce_norm(mlp, L.wd, Fl, T, XP,
+                                         l + 1 < c.num_layers ? layers[l + 1].in_norm : final_norm));
+        else TRY(rowpar_gemm_allreduce(mlp, L.wd, Fl, proj, T, XP));
         ar_drop_now = false;
         prof_end(pr, ALLREDUCE, gemm_bytes(T, H, H, Fl), 2.0 * T * H * Fl);
         mk();
       }
-      if (dbg) TRY(dbg_gemm_out(FFMI_DBG_DOWN, l, proj, down_part, T));
+      if (dbg && !arn) TRY(dbg_gemm_out(FFMI_DBG_DOWN, l, proj, down_part, T));
     }
     const int XP = (packed ? FFMI_X_PACKED : 0) | wstream;
     // (markers also between the tail's kernels: final norm, lm_head, sampling)
@@ -1081,16 +1150,18 @@ struct LlamaGPU : public ffmi_model {
     auto mkt = [&]() {
       if (tail_mark) (void)ffmi::launch_marker(mark_i++, stream);
     };
-    pr = prof_begin(ptail);
-    if (fuse)  // res already holds the last residual add
-      FFMI_HIP(ffmi::launch_rmsnorm(res, nullptr, final_norm, nullptr, h, T, H, eps, stream, packed));
-    else
-      FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
-                                    down_part));
-    prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+    if (!arn) {  // (arn: the last down all-reduce applied the final norm)
+      pr = prof_begin(ptail);
+      if (fuse)  // res already holds the last residual add
+        FFMI_HIP(ffmi::launch_rmsnorm(res, nullptr, final_norm, nullptr, h, T, H, eps, stream, packed));
+      else
+        FFMI_HIP(ffmi::launch_rmsnorm(res, proj, final_norm, res, h, T, H, eps, stream, packed,
+                                      down_part));
+      prof_end(pr, NORM, (double)T * H * 2 * 4, 0);
+    }
     mkt();
     if (dbg) {
-      TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers - 1, res, T));
+      if (!arn) TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers - 1, res, T));
       TRY(dbg_copy(FFMI_DBG_HIDDEN, c.num_layers, h, T));
       dbg_T = T;
     }

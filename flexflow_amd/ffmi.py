@@ -165,6 +165,8 @@ SIGNATURES = {
     "ffmi_vocab_shard_topk": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p,
                                       c_void_p, c_void_p, c_void_p]),
     "ffmi_allreduce": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_int, c_void_p]),
+    "ffmi_allreduce_rmsnorm": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_void_p, c_void_p,
+                                       c_void_p, c_float, c_void_p, c_int, c_void_p, c_void_p]),
     "ffmi_embedding": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_void_p]),
     "ffmi_silu_mul": (c_int, [c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ffmi_argmax": (c_int, [c_void_p, c_int, c_int, c_void_p, c_void_p, c_void_p]),

@@ -277,6 +277,24 @@ ffmi_status ffmi_comm_peer_status(ffmi_comm *c);
 /* Stop using the transport (RCCL again): for a control plane that saw some
  * rank fail its attach -- every rank must take the same transport. */
 ffmi_status ffmi_comm_peer_detach(ffmi_comm *c);
+/* All-reduce fused with the residual RMSNorm after it (the reference's
+ * AllReduce -> ResidualRMSNorm pair of every TP layer, model.cc:3421-3470,
+ * allreduce_kernels.cu:53-75 + residual_rms_norm_kernels.cu:98-131), ONE
+ * kernel over an attached xGMI transport: `in` is this rank's f16 partial of
+ * columns [col0, H) of the [T][H] sum ([T][H - col0], contiguous); columns
+ * [0, col0) of the sum are read from `prev` ([T][H], e.g. an earlier
+ * ffmi_allreduce of those columns; NULL when col0 == 0).  Then, as
+ * ffmi_rmsnorm_ex(residual, sum, w, residual, out, ..., flags):
+ * residual = half(residual + sum) in place and out = RMSNorm(residual) * w
+ * (FFMI_Y_PACKED: packed activation tiles) -- bit-identical to the unfused
+ * pair.  When the transport takes T*H*2 bytes in two shots (> 2 ranks, above
+ * its threshold), rank r normalises only rows [T*r/N, T*(r+1)/N) and gathers
+ * every other rank's rows of `out`: `out` is complete on every rank,
+ * `residual` is updated on this rank's rows only.  rows_out (optional, [2])
+ * receives the updated row range. */
+ffmi_status ffmi_allreduce_rmsnorm(ffmi_comm *c, const void *in, int T, int H, int col0,
+                                   const void *prev, void *residual, const void *w, float eps,
+                                   void *out, int flags, int *rows_out, ffmi_stream stream);
 
 /* ------------------------------------------------------------------------ */
 /* Auxiliary ops on the LLaMA greedy path                                    */

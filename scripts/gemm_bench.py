@@ -20,7 +20,11 @@ SHAPES = {
                 ("down", 4096, 11008, 0), ("lm_head", 32000, 4096, 0)],
     "ssm": [("qkv", 2304, 768, 0), ("o", 768, 768, 0), ("gate_up", 3072, 768, 1),
             ("down", 768, 3072, 0), ("lm_head", 32000, 768, 0)],
-    # per-rank shards of tensor parallelism (TP = 8)
+    # per-rank shards of tensor parallelism (TP = 2, 4, 8)
+    "llama7b_tp2": [("qkv", 6144, 4096, 0), ("o", 4096, 2048, 0), ("gate_up", 5504, 4096, 1),
+                    ("down", 4096, 5504, 0)],
+    "llama7b_tp4": [("qkv", 3072, 4096, 0), ("o", 4096, 1024, 0), ("gate_up", 2752, 4096, 1),
+                    ("down", 4096, 2752, 0)],
     "llama7b_tp8": [("qkv", 1536, 4096, 0), ("o", 4096, 512, 0), ("gate_up", 1376, 4096, 1),
                     ("down", 4096, 1376, 0)],
     "llama65b_tp8": [("qkv", 3072, 8192, 0), ("o", 8192, 1024, 0), ("gate_up", 2752, 8192, 1),

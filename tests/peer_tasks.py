@@ -29,6 +29,51 @@ def ar_task(fa, comm, rank, n, cases, iters):
     return out
 
 
+def arnorm_task(fa, comm, rank, n, cases, seed, iters=2):
+    """ffmi_allreduce_rmsnorm against ffmi_allreduce + ffmi_rmsnorm_ex on the
+    same inputs, per case (T, H, col0, packed): the normalised rows `out` on
+    every row and the residual on the rows the call reports as updated.
+    Columns < col0 come from `prev` = the unfused all-reduce's sum."""
+    import ctypes
+
+    import flexflow_amd.ffmi as F
+    from hip_util import Buf, f16, sync
+    L = F.lib()
+    out = []
+    for it in range(iters):
+        for ci, (T, H, col0, packed) in enumerate(cases):
+            rng = np.random.default_rng(seed + 7919 * ci + 104729 * it)  # same on every rank
+            res0 = f16(rng.standard_normal((T, H)) * 2)
+            w = f16(rng.uniform(0.25, 2.0, H))
+            parts = [f16(rng.standard_normal((T, H)) * 0.7) for _ in range(n)]
+            flags = F.Y_PACKED if packed else 0
+            hbytes = L.ffmi_packed_activation_bytes(T, H) if packed else T * H * 2
+            eps = 1e-5
+            s = Buf(parts[rank])
+            F.check(L.ffmi_allreduce(comm.handle, s.ptr, s.ptr, T * H, F.F16, None), "allreduce")
+            wb = Buf(w)
+            r1, h1 = Buf(res0), Buf.empty((hbytes // 2,), np.uint16)
+            F.check(L.ffmi_rmsnorm_ex(r1.ptr, s.ptr, wb.ptr, r1.ptr, h1.ptr, T, H, eps, flags, None),
+                    "rmsnorm")
+            inp = Buf(np.ascontiguousarray(parts[rank][:, col0:]))
+            r2, h2 = Buf(res0), Buf.empty((hbytes // 2,), np.uint16)
+            rows = (ctypes.c_int * 2)()
+            F.check(L.ffmi_allreduce_rmsnorm(comm.handle, inp.ptr, T, H, col0,
+                                             s.ptr if col0 else None, r2.ptr, wb.ptr, eps, h2.ptr,
+                                             flags, rows, None), "allreduce_rmsnorm")
+            sync()
+            a, b = r1.get().reshape(T, H), r2.get().reshape(T, H)
+            lo, hi = rows[0], rows[1]
+            out.append(dict(case=ci, it=it, rows=(lo, hi),
+                            h_equal=bool(np.array_equal(h1.get(), h2.get())),
+                            res_equal=bool(np.array_equal(a[lo:hi].view(np.uint16),
+                                                          b[lo:hi].view(np.uint16))),
+                            res_others_untouched=bool(np.array_equal(
+                                np.delete(b, np.s_[lo:hi], 0).view(np.uint16),
+                                np.delete(res0, np.s_[lo:hi], 0).view(np.uint16)))))
+    return out
+
+
 def expected_sum(case, it, n, count, dtype):
     acc = np.zeros(count, np.float32)
     for r in range(n):  # rank order, fp32, rounded once

@@ -45,6 +45,31 @@ def test_peer_allreduce_silent_peer_times_out():
     assert r0["seconds"] < 30, r0
 
 
+# (T, H, col0, packed): a decode row, ragged rows, rows fewer than ranks (a
+# rank owning none in two-shot mode), the LLaMA-7B verify batch in column
+# halves, LLaMA-65B width, beyond one chunk per thread (H 16384)
+ARN_CASES = [(1, 256, 0, False), (7, 512, 256, True), (3, 1024, 0, True), (21, 4096, 0, True),
+             (168, 4096, 2048, True), (37, 8192, 4096, False), (5, 16384, 8192, False)]
+
+
+@pytest.mark.parametrize("n,two_shot", [(2, False), (4, False), (4, True), (8, True)])
+def test_peer_allreduce_rmsnorm_fused_equals_unfused(n, two_shot):
+    """The all-reduce with the residual RMSNorm folded into it (model.cc:
+    3421-3470; residual_rms_norm_kernels.cu:98-131) is bit-identical to the
+    transport's all-reduce followed by the norm kernel: the normalised rows on
+    every rank, the residual on the rows the rank updated (its T/N share in
+    two-shot mode, every row in one-shot mode), other rows untouched; two
+    rounds, so the epochs and buffer parities cycle."""
+    env = {"FFMI_PEER_TWO_SHOT_MIN": "0" if two_shot else str(1 << 40)}
+    res = run_group(n, PT.arnorm_task, (ARN_CASES, 99), env=env, max_bytes=2 << 20)
+    for r in range(n):
+        for c in res[r]:
+            T = ARN_CASES[c["case"]][0]
+            want = (T * r // n, T * (r + 1) // n) if two_shot else (0, T)
+            assert tuple(c["rows"]) == want, (r, c)
+            assert c["h_equal"] and c["res_equal"] and c["res_others_untouched"], (r, c)
+
+
 CFG4 = dict(num_layers=2, vocab_size=1000, num_heads=4, num_kv_heads=4, hidden=256,
             intermediate=512, rms_eps=1e-6, rope_theta=10000.0)
 
@@ -89,6 +114,36 @@ def test_peer_tp_model_decodes_like_unsharded(tp, overlap, cfg):
         assert len(toks) == 56
         check_tokens_vs_oracle(cfg, 11, toks, len(p) + 1, tie_ulp=2 * tp,
                                max_tie_frac=0.1)
+
+
+@pytest.mark.parametrize("tp,two_shot,overlap", [(2, False, "1"), (4, True, "1"), (4, True, "0"),
+                                                (4, False, "1"), (8, True, "1")])
+def test_peer_tp_fused_norm_equals_unfused(tp, two_shot, overlap):
+    """TP shards over the transport with every residual norm folded into the
+    all-reduce before it (FFMI_TP_FUSED_NORM, default on; two-shot: each rank
+    normalises its T/TP rows and the rows are gathered) against the separate
+    norm kernel: identical tokens in incremental decoding and SpecInfer, and
+    bit-identical teacher-forced logits (the debug capture, fused with
+    FFMI_TP_FUSED_NORM=2)."""
+    from test_gpu_e2e import SSM_CFG, prompts
+    cfg = CFG4V if tp < 8 else dict(CFG4V, num_heads=8, num_kv_heads=8, hidden=512)
+    ps = prompts(3, cfg["vocab_size"], 4, 30, 13)
+    ts = {"FFMI_PEER_TWO_SHOT_MIN": "0" if two_shot else str(1 << 40), "FFMI_TP_OVERLAP": overlap}
+    ssm = dict(SSM_CFG, vocab_size=cfg["vocab_size"])
+    got = {}
+    for fused in ("0", "2"):
+        env = dict(ts, FFMI_TP_FUSED_NORM=fused)
+        inc = run_group(tp, PT.tp_generate_task, (cfg, 11, ps, 48, False, ssm), env=env,
+                        max_bytes=1 << 20)
+        spec = run_group(tp, PT.model_task, (cfg, 11, ps, 48, True, ssm), env=env,
+                         max_bytes=1 << 20)
+        got[fused] = (inc, spec)
+    (i0, s0), (i2, s2) = got["0"], got["2"]
+    for r in range(tp):
+        assert i2[r]["tokens"] == i0[r]["tokens"] == i0[0]["tokens"], r
+        assert s2[r] == s0[r] == s0[0], r
+        np.testing.assert_array_equal(i2[r]["tf_logits"].view(np.uint16),
+                                      i0[r]["tf_logits"].view(np.uint16), err_msg=f"rank {r}")
 
 
 OFF = int(os.environ.get("FFMI_RANDOM_SEED_OFFSET", "0"))  # fresh seeds for one-off sweeps
