@@ -491,14 +491,14 @@ static hipError_t run(const uint16_t *X, const uint16_t *Wp, uint16_t *Y, float 
 // The K-split form launches 1000 short 4-wave workgroups whose loads never
 // fill the CU (13 us for 49 MB from the Infinity Cache); here each wave keeps
 // two batches of UB k-steps in flight (double-buffered registers).
-template <int MT, int NT, int UB, bool NTL>
-__global__ __launch_bounds__(256) void gemm_wave_kernel(const uint16_t *__restrict__ X,
-                                                        const uint16_t *__restrict__ Wp,
-                                                        uint16_t *__restrict__ Y, int T, int N,
-                                                        int KT, int NTILES, int xp, int yp,
-                                                        size_t wts, size_t wks) {
+template <int MT, int NT, int UB, bool NTL, int WPG = 4>
+__global__ __launch_bounds__(WPG * 64) void gemm_wave_kernel(const uint16_t *__restrict__ X,
+                                                             const uint16_t *__restrict__ Wp,
+                                                             uint16_t *__restrict__ Y, int T, int N,
+                                                             int KT, int NTILES, int xp, int yp,
+                                                             size_t wts, size_t wks) {
   const int lane = threadIdx.x & 63;
-  const int g = blockIdx.x * 4 + (threadIdx.x >> 6);
+  const int g = blockIdx.x * WPG + (threadIdx.x >> 6);
   if (g * NT >= NTILES) return;
   const int XS = xp ? 512 : 32;
   const uint16_t *xrow[MT];
@@ -639,12 +639,33 @@ static hipError_t dispatch_nt(const uint16_t *X, const uint16_t *Wp, uint16_t *Y
     // two tiles per wave: SSM lm_head (32000 x 768) at T = 24 11.1 us (13.3
     // in the K-split form, 13.3 with one tile per wave and twice the waves),
     // T = 8 9.4 us (12.5)
-    const int groups = (ntiles + 1) / 2;
-#define FFMI_WAVE(NL)                                                                      \
-  hipLaunchKernelGGL((gemm_wave_kernel<MT, 2, 4, NL>), dim3((groups + 3) / 4), dim3(256), 0, s, \
-                     X, Wp, Y, T, N, KT, ntiles, xp, yp, wts, wks)
-    if (nt) FFMI_WAVE(true);
-    else FFMI_WAVE(false);
+    // (FFMI_WAVE_FORM=NT,WPG: tiles per wave and waves per workgroup, A/B)
+    static int wnt = 2, wpg = 4;
+    static bool wread = false;
+    if (!wread) {
+      wread = true;
+      if (const char *e = getenv("FFMI_WAVE_FORM")) (void)sscanf(e, "%d,%d", &wnt, &wpg);
+    }
+#define FFMI_WAVE(NTV, WPGV, NL)                                                               \
+  hipLaunchKernelGGL((gemm_wave_kernel<MT, NTV, 4, NL, WPGV>),                                 \
+                     dim3(((ntiles + NTV - 1) / NTV + WPGV - 1) / WPGV), dim3(WPGV * 64), 0, s, X, \
+                     Wp, Y, T, N, KT, ntiles, xp, yp, wts, wks)
+    if (wnt == 4 && wpg == 2) {
+      if (nt) FFMI_WAVE(4, 2, true);
+      else FFMI_WAVE(4, 2, false);
+    } else if (wnt == 4 && wpg == 4) {
+      if (nt) FFMI_WAVE(4, 4, true);
+      else FFMI_WAVE(4, 4, false);
+    } else if (wnt == 3 && wpg == 2) {
+      if (nt) FFMI_WAVE(3, 2, true);
+      else FFMI_WAVE(3, 2, false);
+    } else if (wnt == 2 && wpg == 2) {
+      if (nt) FFMI_WAVE(2, 2, true);
+      else FFMI_WAVE(2, 2, false);
+    } else {
+      if (nt) FFMI_WAVE(2, 4, true);
+      else FFMI_WAVE(2, 4, false);
+    }
 #undef FFMI_WAVE
     return hipGetLastError();
   }

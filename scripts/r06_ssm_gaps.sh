@@ -7,6 +7,9 @@ set -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"; mkdir -p gpurun_out/tl
 export TMPDIR=/tmp
+# (graph packets one by one: the tracer faults in hipGraphLaunch otherwise,
+# DESIGN.md §6 -- so the boundaries are those of packet-by-packet submission)
+export DEBUG_CLR_GRAPH_PACKET_CAPTURE=0
 timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d gpurun_out/tl -o bench -- \
   python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-incr --no-legs --profile 0 \
   > gpurun_out/tl/bench.log 2>&1 || { tail -5 gpurun_out/tl/bench.log; exit 1; }
