@@ -1096,7 +1096,13 @@ static MidPlan mid_plan(int T, int N, int K, int epi, bool deferred = false) {
       // deferred read (norm / attention prologue) is no cheaper than the
       // reduce pass's: /6 had picked 8 slabs for LLaMA-7B o_proj at T = 168,
       // 4 tiles x 4 slabs ran 0.6 % faster end to end (3 of 3 A/B pairs)
-      if (S > 1) t += deferred ? slab_mb / 3.0 : 3.0 + slab_mb / 3.0;
+      // (the SiLU reduce pass re-reads the gate AND up slabs: at the verify
+      // size, 9-12 row tiles in one block, a forced-plan sweep of the TP = 8
+      // gate/up shard put 4 tiles x 4-5 slabs at 18.4-18.9 us against 21.7
+      // for the 6 x 8 the /3 charge picked, profiles/r06_tp8_gateup_plans.log;
+      // the TP 1 / 2 / 4 and 65B TP 8 picks are unchanged by /2)
+      const double slab_rate = epi && p.MTW == 3 && p.mblocks == 1 ? 2.0 : 3.0;
+      if (S > 1) t += deferred ? slab_mb / 3.0 : 3.0 + slab_mb / slab_rate;
       if (t < best - 1e-9) best = t, p.NTW = ntw, p.S = S;
     }
   }
