@@ -846,6 +846,19 @@ struct LlamaGPU : public ffmi_model {
   // and eager steps agree
   int tree_parity = 0;
   std::map<GraphKey, hipGraphExec_t> graphs;
+  // FFMI_CHAIN_GROUP=g (>= 2): chained beam slots 1 .. kChain-2 are staged and
+  // go out g per graph launch (slot kChain-1 alone, behind the collect event):
+  // the boundary between two graph launches (4.9 us from one step's last
+  // kernel to the next step's first, profiles/r06_ssm_gaps.log) becomes a
+  // kernel boundary inside one graph.  1 = one launch per slot.
+  int chain_group = getenv("FFMI_CHAIN_GROUP") ? atoi(getenv("FFMI_CHAIN_GROUP")) : 1;
+  struct PendingSlot {
+    int slot, T, k;
+    size_t bytes;
+    GraphKey key;
+  };
+  std::vector<PendingSlot> pend;  // staged, not yet launched (grouped slots)
+  std::map<std::vector<GraphKey>, hipGraphExec_t> group_graphs;
   bool use_graphs = getenv("FFMI_NO_GRAPHS") == nullptr;
   bool blob_fetch = !getenv("FFMI_BLOB_FETCH") || atoi(getenv("FFMI_BLOB_FETCH")) != 0;
   // largest one-item-per-request step that is graphed (FFMI_GRAPH_MAXT: A/B)
@@ -915,7 +928,7 @@ struct LlamaGPU : public ffmi_model {
         if (graphs.size() >= 512) clear_graphs();
         hipGraph_t g = nullptr;
         FFMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
-        st = enqueue(k, bytes, false);
+        st = enqueue(k, bytes, false, T);
         const hipError_t ce = hipStreamEndCapture(stream, &g);
         if (st != FFMI_OK || ce != hipSuccess) {
           if (g) (void)hipGraphDestroy(g);
@@ -932,13 +945,72 @@ struct LlamaGPU : public ffmi_model {
       FFMI_HIP(hipGraphLaunch(it->second, stream));
     } else {
       if (step_timing) FFMI_HIP(hipEventRecord(st_ev[0], stream));
-      st = enqueue(k, bytes, true);
+      st = enqueue(k, bytes, true, T);
       if (st != FFMI_OK) return st;
     }
     if (step_timing) {
       FFMI_HIP(hipEventRecord(st_ev[1], stream));
       st_t1 = now_us();
     }
+    inflight = true;
+    return FFMI_OK;
+  }
+
+  // A chained slot staged for a grouped launch (chain_group): the staging
+  // half of forward_launch; flush_pending captures / replays the group.
+  ffmi_status stage_pending(int k, int slot) {
+    const int T = (int)ps.tokens.size();
+    ffmi_batch_desc desc;
+    ps.desc(&desc);
+    const long prev_n = slot > 0 ? (long)slot_results[slot - 1] : 0;
+    for (int t = 0; t < T; ++t)
+      FFMI_CHECK((desc.tokens[t].token_id >= 0 && desc.tokens[t].token_id < c.vocab_size) ||
+                     (desc.tokens[t].token_id < 0 && -1L - desc.tokens[t].token_id < prev_n),
+                 FFMI_ERR_INVALID);
+    size_t bytes = 0;
+    ffmi_status st = ffmi::batch_stage(batch, &desc, &bytes);
+    if (st != FFMI_OK) return st;
+    pend.push_back({slot, T, k, bytes,
+                    GraphKey{T, batch->num_work, batch->num_commits, k, tree_parity,
+                             batch->commit_overlap ? 1 : 0,
+                             (batch->one_item_per_req ? 1 : 0) | (batch->lds_tail ? 2 : 0),
+                             batch->max_q, slot, bytes}});
+    return FFMI_OK;
+  }
+  ffmi_status flush_pending() {
+    if (pend.empty()) return FFMI_OK;
+    std::vector<GraphKey> keys;
+    for (const auto &q : pend) keys.push_back(q.key);
+    auto it = group_graphs.find(keys);
+    if (it == group_graphs.end()) {
+      if (group_graphs.size() >= 256) clear_graphs();
+      hipGraph_t g = nullptr;
+      ffmi_status st = FFMI_OK;
+      FFMI_HIP(hipStreamBeginCapture(stream, hipStreamCaptureModeThreadLocal));
+      for (const auto &q : pend) {
+        cur_slot = q.slot;
+        batch = chain_batch[q.slot];
+        st = enqueue(q.k, q.bytes, false, q.T);
+        if (st != FFMI_OK) break;
+      }
+      cur_slot = 0;
+      batch = chain_batch[0];
+      const hipError_t ce = hipStreamEndCapture(stream, &g);
+      if (st != FFMI_OK || ce != hipSuccess) {
+        if (g) (void)hipGraphDestroy(g);
+        pend.clear();
+        if (st != FFMI_OK) return st;
+        FFMI_HIP(ce);
+      }
+      hipGraphExec_t ex = nullptr;
+      const hipError_t ie = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+      (void)hipGraphDestroy(g);
+      if (ie != hipSuccess) pend.clear();
+      FFMI_HIP(ie);
+      it = group_graphs.emplace(keys, ex).first;
+    }
+    pend.clear();
+    FFMI_HIP(hipGraphLaunch(it->second, stream));
     inflight = true;
     return FFMI_OK;
   }
@@ -973,11 +1045,12 @@ struct LlamaGPU : public ffmi_model {
   void clear_graphs() {
     for (auto &kv : graphs) (void)hipGraphExecDestroy(kv.second);
     graphs.clear();
+    for (auto &kv : group_graphs) (void)hipGraphExecDestroy(kv.second);
+    group_graphs.clear();
   }
 
   // everything a step puts on the stream (no host synchronisation inside)
-  ffmi_status enqueue(int k, size_t blob_bytes, bool record_upload) {
-    const int T = (int)ps.tokens.size();
+  ffmi_status enqueue(int k, size_t blob_bytes, bool record_upload, int T) {
     const int H = c.hidden, V = c.vocab_size;
     const float eps = c.rms_eps;
     const ffmi_stream s = (ffmi_stream)stream;
@@ -1271,7 +1344,27 @@ struct LlamaGPU : public ffmi_model {
     batch = chain_batch[slot];
     slot_results[slot] = (size_t)bc.num_tokens * k;
     beam_result_layout(bc, &slot_map[slot]);
-    ffmi_status st = forward_launch(k);
+    // grouped (chain_group): slots 1 .. kChain-2 staged, launched g at a time
+    // (graphed shapes only; anything else first launches what is staged)
+    const int Ts = (int)ps.tokens.size();
+    const bool grp = chain_group >= 2 && slot >= 1 && slot <= kChain - 2 && use_graphs && !dbg &&
+                     prof_level == 0 && Ts > 0 && Ts <= 64;
+    ffmi_status st;
+    if (grp) {
+      st = stage_pending(k, slot);
+      if (st == FFMI_OK && ((slot - 1) % chain_group == chain_group - 1 || slot == kChain - 2)) {
+        cur_slot = 0;
+        batch = chain_batch[0];
+        st = flush_pending();
+      }
+    } else {
+      cur_slot = 0;
+      batch = chain_batch[0];
+      st = flush_pending();
+      cur_slot = slot;
+      batch = chain_batch[slot];
+      if (st == FFMI_OK) st = forward_launch(k);
+    }
     batch = chain_batch[0];
     cur_slot = 0;
     // Events let the scheduler replay slot d's bookkeeping while later slots
@@ -1296,6 +1389,10 @@ struct LlamaGPU : public ffmi_model {
   }
   ffmi_status beam_collect_chained(int slot, BeamInferenceResult *ir) override {
     FFMI_CHECK(slot >= 0 && slot < kChain, FFMI_ERR_INVALID);
+    {  // (grouped slots still staged go out first)
+      ffmi_status st = flush_pending();
+      if (st != FFMI_OK) return st;
+    }
     int ev = -1;  // the first live event at or after this slot, before the last
     for (int e = slot; e < last_slot && ev < 0; ++e)
       if (slot_ev_live[e] && slot_ev[e]) ev = e;

@@ -129,7 +129,8 @@ def test_graph_replay_equals_eager(monkeypatch, ssm):
         assert with_graphs[0] == with_graphs[1]  # SpecInfer == incr decoding
 
 
-@pytest.mark.parametrize("case", ["small", "same", "two_ssms", "queued", "eager"])
+@pytest.mark.parametrize("case", ["small", "same", "two_ssms", "queued", "eager", "group3",
+                                  "group6_two_ssms", "group2_queued"])
 def test_chained_ssm_steps_equal_stepwise(monkeypatch, case):
     """The speculation phase as chained beam steps (8 steps staged up front
     and launched back to back; each step's embedding gather takes its tokens
@@ -138,24 +139,27 @@ def test_chained_ssm_steps_equal_stepwise(monkeypatch, case):
     results, trees, verify batches and tokens must be IDENTICAL, and so must
     every step count.  Cases: the small SSM, SSM == LLM weights (long accepted
     paths), two SSMs with merged trees, more requests than slots (prompts
-    loading beside running requests), and eager steps (FFMI_NO_GRAPHS)."""
+    loading beside running requests), eager steps (FFMI_NO_GRAPHS), and the
+    chained slots launched several per graph (FFMI_CHAIN_GROUP)."""
     cfg, seed = LLM_CFG, 41
-    n, batch = (8, 4) if case == "queued" else (4, 4)
+    n, batch = (8, 4) if case.endswith("queued") else (4, 4)
     ps = prompts(n, cfg["vocab_size"], 5, 40, seed)
     if case == "eager":
         monkeypatch.setenv("FFMI_NO_GRAPHS", "1")
+    if case.startswith("group"):
+        monkeypatch.setenv("FFMI_CHAIN_GROUP", case[5])
 
     def run(chain):
         monkeypatch.setenv("FFMI_SSM_CHAIN", "1" if chain else "0")
         vt = 64 + 23 * batch
-        ext = fa.ffmi.SPEC_EXT_MULTI_SSM if case == "two_ssms" else 0
+        ext = fa.ffmi.SPEC_EXT_MULTI_SSM if case.endswith("two_ssms") else 0
         rm = fa.RequestManager(max_requests_per_batch=batch, max_tokens_per_batch=64,
                                max_sequence_length=128, spec_tree_width=(1, 1, 3),
                                max_spec_tree_token_num=23, spec_extensions=ext)
         llm = fa.Model(cfg, "tree", max_requests=batch, max_tokens=vt, max_seq_len=128,
                        max_tree_tokens=23, weight_seed=seed)
         drafts = [(SSM_CFG, 5)] if case != "same" else [(cfg, seed)]
-        if case == "two_ssms":
+        if case.endswith("two_ssms"):
             drafts.append((SSM_CFG, 6))
         models = [fa.Model(c, "beam", max_requests=batch, max_tokens=vt, max_seq_len=128,
                            max_tree_tokens=23, weight_seed=sd) for c, sd in drafts]
