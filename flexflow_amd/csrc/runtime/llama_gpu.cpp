@@ -850,8 +850,12 @@ struct LlamaGPU : public ffmi_model {
   // go out g per graph launch (slot kChain-1 alone, behind the collect event):
   // the boundary between two graph launches (4.9 us from one step's last
   // kernel to the next step's first, profiles/r06_ssm_gaps.log) becomes a
-  // kernel boundary inside one graph.  1 = one launch per slot.
-  int chain_group = getenv("FFMI_CHAIN_GROUP") ? atoi(getenv("FFMI_CHAIN_GROUP")) : 1;
+  // kernel boundary inside one graph.  1 = one launch per slot.  Default: all
+  // six middle slots in one launch (the host stages them while slot 0 runs).
+  // Same box, 3 pairs (profiles/r06_chain_group_ab.log): SSM step 95.8-97.8
+  // (1 per launch) -> 93.8-94.5 (3) -> 92.9-93.9 us (6); 1325-1330 -> 1332-1336
+  // tokens/s
+  int chain_group = getenv("FFMI_CHAIN_GROUP") ? atoi(getenv("FFMI_CHAIN_GROUP")) : kChain - 2;
   struct PendingSlot {
     int slot, T, k;
     size_t bytes;

@@ -130,7 +130,7 @@ def test_graph_replay_equals_eager(monkeypatch, ssm):
 
 
 @pytest.mark.parametrize("case", ["small", "same", "two_ssms", "queued", "eager", "group3",
-                                  "group6_two_ssms", "group2_queued"])
+                                  "group1_two_ssms", "group2_queued"])
 def test_chained_ssm_steps_equal_stepwise(monkeypatch, case):
     """The speculation phase as chained beam steps (8 steps staged up front
     and launched back to back; each step's embedding gather takes its tokens
@@ -140,7 +140,8 @@ def test_chained_ssm_steps_equal_stepwise(monkeypatch, case):
     every step count.  Cases: the small SSM, SSM == LLM weights (long accepted
     paths), two SSMs with merged trees, more requests than slots (prompts
     loading beside running requests), eager steps (FFMI_NO_GRAPHS), and the
-    chained slots launched several per graph (FFMI_CHAIN_GROUP)."""
+    chained slots' grouping per graph launch (FFMI_CHAIN_GROUP: default all six
+    middle slots in one launch; 1, 2 and 3 here)."""
     cfg, seed = LLM_CFG, 41
     n, batch = (8, 4) if case.endswith("queued") else (4, 4)
     ps = prompts(n, cfg["vocab_size"], 5, 40, seed)
