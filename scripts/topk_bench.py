@@ -15,7 +15,7 @@ from hip_util import Buf, Timer, f16  # noqa: E402
 
 L = F.lib()
 rng = np.random.default_rng(0)
-for T, V, k in [(24, 32000, 3), (24, 31999, 3), (168, 32000, 1), (8, 32000, 1), (24, 32000, 1),
+for T, V, k in [(24, 32000, 3), (24, 31999, 3), (168, 32000, 1), (8, 32000, 1), (8, 32000, 3), (24, 32000, 1),
                 (24, 32001, 3), (168, 32001, 1), (24, 128256, 3), (168, 128256, 1)]:
     x = Buf(f16(rng.standard_normal((T, V)) * 3.0))
     ids = Buf.empty((T, k), np.int32)
