@@ -758,7 +758,9 @@ hipError_t launch_argmax(const uint16_t *logits, int T, int V, int k, int32_t *i
   // lm_head GEMM -- 336 workgroups put two on many CUs -- and the verify step
   // 5.30 vs 5.28 ms; off)
   static const bool split2 = getenv("FFMI_TOPK_SPLIT2") && atoi(getenv("FFMI_TOPK_SPLIT2"));
-  int G = T <= 16 ? 16 : T <= 32 ? 8 : T <= 64 ? 4 : T <= 128 ? 2 : (T <= kSplitRows && split2) ? 2 : 1;
+  // (T <= 16 took 16 before: 8 measured 0.5 us faster at T = 8, k 1 and 3,
+  // profiles/r06_topk_g.log)
+  int G = T <= 32 ? 8 : T <= 64 ? 4 : T <= 128 ? 2 : (T <= kSplitRows && split2) ? 2 : 1;
   if (split_env >= 0) G = split_env;
   if (!ws || ws_bytes < argmax_workspace_bytes(T) || T > kSplitRows) G = 1;
   unsigned *cnt = reinterpret_cast<unsigned *>(ws);
