@@ -600,7 +600,9 @@ static hipError_t dispatch_fused(const uint16_t *X, const uint16_t *Wp, uint16_t
                                     wpitch, fz);
     return hipErrorInvalidValue;
   }
-  if (MT >= 2 && ntiles >= 512)
+  // FFMI_FZ_NT2=1: two tiles per workgroup at one row tile too (A/B)
+  static const bool nt2 = getenv("FFMI_FZ_NT2") && atoi(getenv("FFMI_FZ_NT2")) != 0;
+  if ((MT >= 2 || nt2) && ntiles >= 512)
     return run<MT, 2, 4, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
   if (ntiles < 512 && KT >= 64 && !nt)
     return run<MT, 1, 8, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
