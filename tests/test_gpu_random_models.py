@@ -145,6 +145,67 @@ def test_random_model_spec_infer_vs_oracle(seed):
     check_all(cfg, 200 + seed, ps, res, ml, (cfg, B, mtb, widths, nssm))
 
 
+@pytest.mark.parametrize("seed", range(max(1, SEEDS // 2)))
+def test_random_model_chained_ssm_steps_equal_stepwise(seed, monkeypatch):
+    """The chained speculation phase (beam steps staged from placeholder
+    results, the middle steps grouped into one graph launch -- FFMI_CHAIN_GROUP
+    drawn at random) against the stepwise loop (FFMI_SSM_CHAIN=0) on a random
+    model and request mix: identical tokens and identical step, commit and
+    tree-token counts (the same kernels on the same inputs)."""
+    rng = np.random.default_rng(9700 + OFF + seed)
+    cfg = random_cfg(rng)
+    V = cfg["vocab_size"]
+    msl = int(rng.choice([64, 128, 256]))
+    ps, ml = random_requests(rng, V, msl)
+    B = int(rng.choice([1, 2, 4, 8]))
+    mtb = int(rng.choice([32, 64, 128]))
+    widths = WIDTHS[int(rng.integers(0, len(WIDTHS) - 1))]  # (not incr decoding)
+    nssm = int(rng.integers(1, 3))
+    tree = 64 if nssm > 1 else 33
+    ext = fa.ffmi.SPEC_EXT_WIDTH4 | (fa.ffmi.SPEC_EXT_MULTI_SSM if nssm > 1 else 0)
+    vt = mtb + tree * B
+    scfgs = []
+    for k in range(nssm):
+        same = rng.random() < 0.3
+        scfgs.append((cfg, 400 + seed) if same else (random_cfg(rng, vocab=V), 500 + k))
+    group = str(int(rng.choice([1, 2, 3, 6])))
+
+    def run(chain):
+        monkeypatch.setenv("FFMI_SSM_CHAIN", "1" if chain else "0")
+        monkeypatch.setenv("FFMI_CHAIN_GROUP", group)
+        rm = fa.RequestManager(max_requests_per_batch=B, max_tokens_per_batch=mtb,
+                               max_sequence_length=msl, spec_tree_width=widths,
+                               max_spec_tree_token_num=tree, spec_extensions=ext)
+        llm = fa.Model(cfg, "tree", max_requests=B, max_tokens=vt, max_seq_len=msl,
+                       max_tree_tokens=tree, weight_seed=400 + seed)
+        ssms = [fa.Model(c, "beam", max_requests=B, max_tokens=vt, max_seq_len=msl,
+                         max_tree_tokens=tree, weight_seed=sd) for c, sd in scfgs]
+        for m in ssms:
+            rm.register_ssm_model(m)
+        try:
+            res = fa.generate(rm, llm, ps, max_length=ml, spec=True)
+        except fa.ffmi.FFMIError as e:  # (as test_random_model_spec_infer_vs_oracle)
+            assert "SSM loaded less" in str(e)
+            return None
+        finally:
+            llm.close()
+            for m in ssms:
+                m.close()
+        st = rm.stats()
+        return [r.output_tokens for r in res], {
+            f: getattr(st, f) for f in ("llm_steps", "ssm_steps", "tokens_committed",
+                                        "tree_tokens_verified", "request_verifies")}, \
+            st.ssm_phases_chained
+
+    a, b = run(False), run(True)
+    if a is None or b is None:
+        assert a is None and b is None
+        pytest.skip("SSM prompt behind the LLM for this random mix")
+    assert a[2] == 0
+    assert b[0] == a[0], (cfg, B, mtb, widths, nssm, group)
+    assert b[1] == a[1], (cfg, B, mtb, widths, nssm, group)
+
+
 def oracle_free_running(cfg, seed, prompt, max_length):
     """the fp32 oracle's own greedy continuation of one prompt (BOS
     included) and its logit rows"""
