@@ -63,6 +63,11 @@ def test_invalid_arguments_return_status_not_abort():
     for mode in (F.ATTN_TREE, F.ATTN_SPEC):
         cfg = F.AttnCfg(mode, 2, 32, 1, 16, 8, 16, 0.1, 10000.0, 0)
         assert L.ffmi_attn_create(ctypes.byref(cfg), ctypes.byref(h)) == 5
+    # the all-reduce + residual norm with null operands
+    assert L.ffmi_allreduce_rmsnorm(None, None, 8, 256, 0, None, None, None, 1e-6, None, 0, None,
+                                    None) == 1
+    # the top-k with a caller workspace: null operands
+    assert L.ffmi_arg_topk_ws(None, 4, 32000, 1, None, None, None, 0, None) == 1
 
 
 def test_full_precision_model_opts_and_no_device():
