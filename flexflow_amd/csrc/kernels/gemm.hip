@@ -594,12 +594,22 @@ static hipError_t dispatch_fused(const uint16_t *X, const uint16_t *Wp, uint16_t
                                  int K, int KT, int epi, hipStream_t s, int xp, int yp, bool nt,
                                  int wpitch, const FuseArgs &fz) {
   const int ntiles = (N + 15) / 16;
+  // FFMI_FZ_KW8 (A/B): 8 K-split waves instead of 4 for the one-row-tile
+  // consumer launches -- 1: qkv, 2: qkv and gate/up
+  static const int kw8 = getenv("FFMI_FZ_KW8") ? atoi(getenv("FFMI_FZ_KW8")) : 0;
   if (epi == FFMI_EPI_SILU_MUL) {
-    if constexpr (FZ == 2)
+    if constexpr (FZ == 2) {
+      if (kw8 >= 2 && MT == 1)
+        return run<MT, 2, 8, U, 1, 2>(X, Wp, Y, nullptr, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt,
+                                      wpitch, fz);
       return run<MT, 2, 4, U, 1, 2>(X, Wp, Y, nullptr, T, N, K, KT, 2 * ntiles, 1, s, xp, yp, nt,
                                     wpitch, fz);
+    }
     return hipErrorInvalidValue;
   }
+  if constexpr (FZ == 2)
+    if (kw8 >= 1 && MT == 1 && ntiles >= 512)
+      return run<MT, 1, 8, U, 0, FZ>(X, Wp, Y, nullptr, T, N, K, KT, ntiles, 1, s, xp, yp, nt, wpitch, fz);
   // FFMI_FZ_NT2=1: two tiles per workgroup at one row tile too (A/B)
   static const bool nt2 = getenv("FFMI_FZ_NT2") && atoi(getenv("FFMI_FZ_NT2")) != 0;
   if ((MT >= 2 || nt2) && ntiles >= 512)
