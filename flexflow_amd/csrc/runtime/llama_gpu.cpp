@@ -609,6 +609,14 @@ struct LlamaGPU : public ffmi_model {
                            hipHostMallocCoherent | hipHostMallocMapped));
     if (mode == FFMI_MODEL_BEAM) TRY(alloc(&ids_dev, (size_t)kChain * Tm * 4));
     chain_batch[0] = batch;
+    // the chained beam steps' staging batches, created here rather than on a
+    // chain's first use: creating one clears its device blob on the legacy
+    // stream, which fails -- and invalidates the capture -- while another
+    // thread's model is capturing a graph (the TP shard threads of one
+    // process, ffmi_comm_create_local, beside their SSMs)
+    if (mode == FFMI_MODEL_BEAM && o.tp_size == 1)
+      for (int i = 1; i < kChain; ++i)
+        TRY(ffmi_batch_create((o.max_tokens + 15) & ~15, o.max_requests, &chain_batch[i]));
     // weights (seeded synthetic, orc_gen_weight spec), packed for MFMA
     uint16_t *tmp = nullptr;
     size_t tmp_elems = std::max((size_t)V * H, std::max((size_t)F * H, (size_t)H * H));
