@@ -54,7 +54,7 @@ hipError_t launch_peer_allreduce(const PeerArgs &a, bool two_shot, hipStream_t s
 
 // All-reduce fused with the residual RMSNorm that follows it
 // (residual_rms_norm_kernels.cu:98-131 after allreduce_kernels.cu:53-75;
-// model.cc:3421-3470).  The all-reduced partial covers columns [col0, H) of
+// model.cc:3421-3445).  The all-reduced partial covers columns [col0, H) of
 // the [T][H] sum (PeerArgs cols = H - col0, f16); columns [0, col0) come from
 // `prev`, the sum of an earlier column chunk (launch_peer_allreduce with
 // rs_rows, or a whole one-shot all-reduce).  For rows [row0, row1):

@@ -95,7 +95,7 @@ struct LlamaGPU : public ffmi_model {
   int oslab_T = 0;
   // the residual norm after each all-reduce folded into it over the transport
   // (ffmi::comm_allreduce_norm; the reference's AllReduce -> ResidualRMSNorm,
-  // model.cc:3421-3470): no norm launch per all-reduce, and in two-shot mode
+  // model.cc:3421-3445): no norm launch per all-reduce, and in two-shot mode
   // each rank normalises only its T / N rows (res is then current on those
   // rows only; h is complete).  FFMI_TP_FUSED_NORM: 0 off, 1 on (not with
   // debug captures), 2 also with debug captures (tests: the h and logits

@@ -278,7 +278,7 @@ ffmi_status ffmi_comm_peer_status(ffmi_comm *c);
  * rank fail its attach -- every rank must take the same transport. */
 ffmi_status ffmi_comm_peer_detach(ffmi_comm *c);
 /* All-reduce fused with the residual RMSNorm after it (the reference's
- * AllReduce -> ResidualRMSNorm pair of every TP layer, model.cc:3421-3470,
+ * AllReduce -> ResidualRMSNorm pair of every TP layer, model.cc:3421-3445,
  * allreduce_kernels.cu:53-75 + residual_rms_norm_kernels.cu:98-131), ONE
  * kernel over an attached xGMI transport: `in` is this rank's f16 partial of
  * columns [col0, H) of the [T][H] sum ([T][H - col0], contiguous); columns
