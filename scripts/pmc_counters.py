@@ -52,7 +52,7 @@ def main(out, prefix, dirs):
                     row[c.replace("_sum", "") + "_per_cu_frac"] = round(avg[c] / n / cyc, 3)
         if "SQ_WAVE_CYCLES" in avg and avg["SQ_WAVE_CYCLES"]:
             w = avg["SQ_WAVE_CYCLES"]
-            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+            for c in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_ACTIVE_INST_VALU"):
                 if c in avg:
                     row[c + "_of_wave_cycles"] = round(avg[c] / w, 3)
         res.append(row)
