@@ -913,6 +913,18 @@ static hipError_t launch_attention_d(const char *blob, int W, int max_q, uint16_
                          s, blob, qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
     return hipGetLastError();
   }
+  // FFMI_ATTN_NW4=1 (A/B): fused one-query-tile launches (decode, SSM beam
+  // steps) with 4 waves per workgroup instead of 8
+  static const bool nw4 = getenv("FFMI_ATTN_NW4") && atoi(getenv("FFMI_ATTN_NW4")) != 0;
+  if (max_q <= 16 && fused && nw4 && D == 128) {
+    if (kv.part)
+      hipLaunchKernelGGL((attention_kernel<D, 1, 4, true, false, 1>), grid, dim3(256), 0, s, blob,
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
+    else
+      hipLaunchKernelGGL((attention_kernel<D, 1, 4, true, false, 0>), grid, dim3(256), 0, s, blob,
+                         qbuf, kc, vc, out, heads, slots, scale, op, kv, OprojArgs());
+    return hipGetLastError();
+  }
   if (max_q <= 16) {
     if (fused) FFMI_ATT(1, true);
     else FFMI_ATT(1, false);
